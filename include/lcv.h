@@ -1,0 +1,150 @@
+/* lcv.h — C ABI of liblcv.so, the MI355X (gfx950) batched light-client verifier.
+ *
+ * Drop-in boundary for the hot path of Inspector-Butters/light-client-consensus-specs:
+ *   validate_light_client_update(store, update, current_slot, genesis_validators_root)
+ *       reference sync-protocol.md:386-465           -> lcv_set_store + lcv_validate_updates
+ *   bls.FastAggregateVerify(pubkeys, message, signature)
+ *       reference call site sync-protocol.md:464      -> lcv_fast_aggregate_verify(_batch)
+ *   is_valid_merkle_branch(leaf, branch, depth, index, root)
+ *       reference call sites sync-protocol.md:234,356,428,443 -> lcv_merkle_branch_batch
+ *   hash_tree_root(SyncCommittee)
+ *       reference call site sync-protocol.md:444      -> lcv_htr_sync_committee_batch
+ *
+ * Conventions: plain pointers and sizes, caller owns every host buffer, the library copies in and
+ * out.  Every function returns 0 (LCV_OK) or a negative lcv_status; lcv_last_error() explains.
+ * No C++ exception crosses the ABI.  One lcv_ctx per device, not shared between threads.
+ * Byte layouts of the packed update batch (structure of arrays, one row per update) are given
+ * next to lcv_update_batch and in DESIGN.md.
+ */
+#ifndef LCV_H
+#define LCV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LCV_SYNC_COMMITTEE_SIZE 512
+#define LCV_PUBKEY_BYTES 48
+#define LCV_SIGNATURE_BYTES 96
+#define LCV_SYNC_COMMITTEE_BYTES 24624 /* SSZ SyncCommittee: 512 x 48 B pubkeys + 48 B aggregate */
+#define LCV_BEACON_HEADER_BYTES 112    /* SSZ BeaconBlockHeader */
+#define LCV_EXEC_RECORD_BYTES 832      /* packed ExecutionPayloadHeader, see below */
+#define LCV_EXEC_BRANCH_BYTES 128      /* ExecutionBranch 4 x 32 */
+#define LCV_NSC_BRANCH_BYTES 160       /* NextSyncCommitteeBranch 5 x 32 */
+#define LCV_FINALITY_BRANCH_BYTES 192  /* FinalityBranch 6 x 32 */
+#define LCV_SYNC_BITS_BYTES 64         /* SSZ Bitvector[512] */
+
+enum lcv_status { LCV_OK = 0, LCV_EINVAL = -1, LCV_EDEVICE = -2, LCV_ENOMEM = -3, LCV_ESTATE = -4 };
+
+/* reason codes: k = the k-th assert of validate_light_client_update in source order */
+enum lcv_reason {
+  LCV_VALID = 0,
+  LCV_R_PARTICIPANTS = 1,            /* :392 */
+  LCV_R_ATTESTED_HEADER = 2,         /* :395 */
+  LCV_R_SLOT_ORDER = 3,              /* :398 */
+  LCV_R_SIG_PERIOD_NEXT_KNOWN = 4,   /* :402 */
+  LCV_R_SIG_PERIOD_NEXT_UNKNOWN = 5, /* :404 */
+  LCV_R_NOT_RELEVANT = 6,            /* :411-414 */
+  LCV_R_FINALIZED_NOT_EMPTY = 7,     /* :420 */
+  LCV_R_FINALIZED_GENESIS = 8,       /* :423 */
+  LCV_R_FINALIZED_HEADER = 9,        /* :426 */
+  LCV_R_FINALITY_BRANCH = 10,        /* :428-434 */
+  LCV_R_NSC_NOT_EMPTY = 11,          /* :439 */
+  LCV_R_NSC_MISMATCH = 12,           /* :442 */
+  LCV_R_NSC_BRANCH = 13,             /* :443-449 */
+  LCV_R_SIGNATURE = 14               /* :464 */
+};
+
+typedef struct lcv_ctx lcv_ctx;
+typedef struct lcv_dbatch lcv_dbatch;
+
+/* Packed ExecutionPayloadHeader record (832 B): 17 SSZ leaf chunks of 32 B in field order
+ * (parent_hash, fee_recipient (20 B + 12 zero), state_root, receipts_root, [leaf 4 unused: zero],
+ * prev_randao, block_number, gas_limit, gas_used, timestamp (uint64 LE + 24 zero),
+ * extra_data (zero padded), base_fee_per_gas (uint256 LE), block_hash, transactions_root,
+ * withdrawals_root, blob_gas_used, excess_blob_gas), then logs_bloom (256 B) at offset 544,
+ * extra_data length (uint32 LE) at 800, 28 zero bytes.  All-zero == ExecutionPayloadHeader(). */
+typedef struct lcv_header_cols {
+  const uint8_t* beacon;      /* n x 112 */
+  const uint8_t* execution;   /* n x 832 */
+  const uint8_t* exec_branch; /* n x 128 */
+} lcv_header_cols;
+
+typedef struct lcv_update_batch {
+  lcv_header_cols attested;
+  lcv_header_cols finalized;
+  const uint8_t* nsc_pool;        /* npool x 24624: distinct next_sync_committee values */
+  const uint32_t* nsc_index;      /* n: pool row holding update i's next_sync_committee */
+  const uint8_t* nsc_branch;      /* n x 160 */
+  const uint8_t* finality_branch; /* n x 192 */
+  const uint8_t* sync_bits;       /* n x 64 */
+  const uint8_t* sync_signature;  /* n x 96 */
+  const uint64_t* signature_slot; /* n */
+  uint64_t n;
+  uint64_t npool;
+} lcv_update_batch;
+
+/* ---- context */
+int lcv_device_count(int* out);
+int lcv_init(int device, lcv_ctx** out);
+void lcv_destroy(lcv_ctx* ctx);
+const char* lcv_last_error(const lcv_ctx* ctx);
+
+/* ---- validate_light_client_update (sync-protocol.md:386-465) against one store snapshot.
+ * The store's two committees (SSZ SyncCommittee bytes; an all-zero next committee means
+ * "not known", sync-protocol.md:316-317) are decoded and KeyValidated once, device resident.
+ * key_status_out (optional, 1024 B): 0 valid key, 2 invalid. */
+int lcv_set_store(lcv_ctx* ctx, uint64_t finalized_slot, const uint8_t* current_sync_committee,
+                  const uint8_t* next_sync_committee, uint8_t* key_status_out);
+/* host batch in, verdict (1 = valid) and reason code (lcv_reason) out, one byte per update */
+int lcv_validate_updates(lcv_ctx* ctx, const lcv_update_batch* batch, uint64_t current_slot,
+                         const uint8_t* genesis_validators_root, uint8_t* verdict_out, uint8_t* reason_out);
+/* device-resident batches: upload once, validate many times (timed region excludes the upload) */
+int lcv_batch_upload(lcv_ctx* ctx, const lcv_update_batch* batch, lcv_dbatch** out);
+void lcv_batch_free(lcv_ctx* ctx, lcv_dbatch* b);
+int lcv_validate_resident(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot, const uint8_t* genesis_validators_root,
+                          uint8_t* verdict_out, uint8_t* reason_out);
+/* same, verdicts written to a DEVICE buffer of n bytes (for an RCCL all-gather); no host copy */
+int lcv_validate_resident_dev(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot,
+                              const uint8_t* genesis_validators_root, uint8_t* verdict_dev);
+/* kernel time of the last validate call: total and per stage (ms); names via lcv_stage_name */
+int lcv_last_timings(lcv_ctx* ctx, float* ms_out, int max_stages, int* nstages);
+const char* lcv_stage_name(int stage);
+
+/* ---- bls.FastAggregateVerify (sync-protocol.md:464); py_ecc semantics (every key KeyValidated) */
+int lcv_fast_aggregate_verify(lcv_ctx* ctx, const uint8_t* pubkeys48, uint64_t npk, const uint8_t* msg32,
+                              const uint8_t* sig96, int* result);
+/* batched: committee table (ncomm x 512 x 48 B), per item committee id + participation bits */
+int lcv_fast_aggregate_verify_batch(lcv_ctx* ctx, const uint8_t* committees, uint64_t ncomm,
+                                    const uint32_t* committee_id, const uint8_t* bits64, const uint8_t* msg32,
+                                    const uint8_t* sig96, uint64_t n, uint8_t* verdict_out);
+
+/* ---- SSZ */
+int lcv_merkle_branch_batch(lcv_ctx* ctx, const uint8_t* leaf32, const uint8_t* branch, uint32_t depth,
+                            uint64_t index, const uint8_t* root32, uint64_t n, uint8_t* out);
+int lcv_htr_sync_committee_batch(lcv_ctx* ctx, const uint8_t* committees, uint64_t n, uint8_t* roots32_out);
+
+/* ---- synthetic-data signer (producer side).  Secret keys 32 B big-endian. */
+int lcv_sk_to_pk_batch(lcv_ctx* ctx, const uint8_t* sk32, uint64_t n, uint8_t* pk48_out);
+int lcv_sign_batch(lcv_ctx* ctx, const uint8_t* sk32, const uint8_t* msg32, uint64_t n, uint8_t* sig96_out);
+
+/* ---- parity-test entry points (intermediate values, canonical big-endian bytes) */
+/* field ops on (a, b) < p: out per item = a*b, a+b, a-b, a^-1, sqrt_fp2(a + b u) (2 x 48); ok = sqrt exists */
+int lcv_debug_fp(lcv_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint64_t n, uint8_t* out288, uint8_t* ok);
+/* hash_to_G2(msg) affine (x0 || x1 || y0 || y1, 4 x 48 B); inf flag */
+int lcv_debug_hash_to_g2(lcv_ctx* ctx, const uint8_t* msg32, uint64_t n, uint8_t* out192, uint8_t* inf);
+/* signature decode + subgroup check: affine point + status (0 ok, 1 identity, 2 invalid) */
+int lcv_debug_g2_decompress(lcv_ctx* ctx, const uint8_t* sig96, uint64_t n, uint8_t* out192, uint8_t* status);
+/* masked aggregate (affine x || y) + status (0 ok, 1 identity, 2 invalid key among participants) */
+int lcv_debug_aggregate(lcv_ctx* ctx, const uint8_t* committees, uint64_t ncomm, const uint32_t* committee_id,
+                        const uint8_t* bits64, uint64_t n, uint8_t* out96, uint8_t* status);
+/* e(P, Q)^3 after final exponentiation (12 x 48 B, coefficient order g0..g5 of w^i, each c0 || c1) */
+int lcv_debug_pairing(lcv_ctx* ctx, const uint8_t* p96, const uint8_t* q192, uint64_t n, uint8_t* out576);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LCV_H */

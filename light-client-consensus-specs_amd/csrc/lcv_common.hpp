@@ -1,0 +1,53 @@
+// lcv_common.hpp — compilation-target macros shared by the HIP build (liblcv.so, gfx950)
+// and the host-simulation test build (liblcv_hostsim.so, g++: the same per-item code run on
+// CPU so that the arithmetic can be checked against the oracle without a GPU).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(LCV_HOSTSIM)
+#define LCV_FN static inline
+#define LCV_NOINLINE static __attribute__((noinline))
+#define LCV_CMEM static const
+#define LCV_UNROLL _Pragma("GCC unroll 64")
+#define LCV_NOUNROLL _Pragma("GCC unroll 1")
+#define LCV_GLOBAL_PTR
+#else
+#include <hip/hip_runtime.h>
+#define LCV_FN __device__ __forceinline__
+#define LCV_NOINLINE __device__ __noinline__
+#define LCV_CMEM static __constant__ const
+#define LCV_UNROLL _Pragma("unroll")
+#define LCV_NOUNROLL _Pragma("unroll 1")
+#endif
+
+// Field multiplication strategy on the device:
+//   LCV_FP_CALL=1 : fp_mul/fp_sqr are real (non-inlined) functions taking the 24 limbs as scalar
+//                   VGPR arguments and returning 12 limbs in VGPRs (keeps kernels I-cache sized);
+//   LCV_FP_CALL=0 : fully inlined everywhere.
+#ifndef LCV_FP_CALL
+#if defined(LCV_HOSTSIM)
+#define LCV_FP_CALL 0
+#else
+#define LCV_FP_CALL 1
+#endif
+#endif
+
+#define LCV_COPY12(dst, src) do { LCV_UNROLL for (int _i = 0; _i < 12; ++_i) (dst)[_i] = (src)[_i]; } while (0)
+
+namespace lcv {
+
+LCV_FN uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+LCV_FN uint32_t ld_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+LCV_FN uint32_t ld_be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+LCV_FN void st_be32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+LCV_FN uint64_t ld_le64(const uint8_t* p) { return (uint64_t)ld_le32(p) | ((uint64_t)ld_le32(p + 4) << 32); }
+
+}  // namespace lcv

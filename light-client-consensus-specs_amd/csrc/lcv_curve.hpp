@@ -1,0 +1,364 @@
+// lcv_curve.hpp — E1(Fp): y^2 = x^3 + 4 (G1, pubkeys) and the twist E2(Fp2): y^2 = x^3 + 4(1+u)
+// (G2, signatures / hash_to_G2).  Jacobian coordinates, complete case handling (P == Q doubling,
+// P == -Q, identity) so that adversarial inputs give the mathematically exact result.
+// ZCash compressed encoding with py_ecc's decoding rules (see oracle/bls12_381.py).
+#pragma once
+#include "lcv_tower.hpp"
+
+namespace lcv {
+
+// ---- overloads so the point code is written once for Fp and Fp2
+LCV_FN void f_add(fp& r, const fp& a, const fp& b) { fp_add(r, a, b); }
+LCV_FN void f_add(fp2& r, const fp2& a, const fp2& b) { fp2_add(r, a, b); }
+LCV_FN void f_sub(fp& r, const fp& a, const fp& b) { fp_sub(r, a, b); }
+LCV_FN void f_sub(fp2& r, const fp2& a, const fp2& b) { fp2_sub(r, a, b); }
+LCV_FN void f_dbl(fp& r, const fp& a) { fp_dbl(r, a); }
+LCV_FN void f_dbl(fp2& r, const fp2& a) { fp2_dbl(r, a); }
+LCV_FN void f_neg(fp& r, const fp& a) { fp_neg(r, a); }
+LCV_FN void f_neg(fp2& r, const fp2& a) { fp2_neg(r, a); }
+LCV_FN void f_mul(fp& r, const fp& a, const fp& b) { fp_mul(r, a, b); }
+LCV_FN void f_mul(fp2& r, const fp2& a, const fp2& b) { fp2_mul(r, a, b); }
+LCV_FN void f_sqr(fp& r, const fp& a) { fp_sqr(r, a); }
+LCV_FN void f_sqr(fp2& r, const fp2& a) { fp2_sqr(r, a); }
+LCV_FN void f_inv(fp& r, const fp& a) { fp_inv(r, a); }
+LCV_FN void f_inv(fp2& r, const fp2& a) { fp2_inv(r, a); }
+LCV_FN bool f_is_zero(const fp& a) { return fp_is_zero(a); }
+LCV_FN bool f_is_zero(const fp2& a) { return fp2_is_zero(a); }
+LCV_FN bool f_eq(const fp& a, const fp& b) { return fp_eq(a, b); }
+LCV_FN bool f_eq(const fp2& a, const fp2& b) { return fp2_eq(a, b); }
+LCV_FN void f_one(fp& r) { fp_one(r); }
+LCV_FN void f_one(fp2& r) { fp2_one(r); }
+
+template <class F> struct jac { F x, y, z; };
+template <class F> struct aff { F x, y; };
+typedef jac<fp> g1j;
+typedef aff<fp> g1a;
+typedef jac<fp2> g2j;
+typedef aff<fp2> g2a;
+
+template <class F> LCV_FN void jac_set_inf(jac<F>& r) { f_one(r.x); f_one(r.y); r.z = r.x; f_sub(r.z, r.z, r.z); }
+template <class F> LCV_FN bool jac_is_inf(const jac<F>& p) { return f_is_zero(p.z); }
+template <class F> LCV_FN void jac_from_aff(jac<F>& r, const aff<F>& a) { r.x = a.x; r.y = a.y; f_one(r.z); }
+template <class F> LCV_FN void jac_neg(jac<F>& r, const jac<F>& p) { r.x = p.x; f_neg(r.y, p.y); r.z = p.z; }
+
+// dbl-2009-l (a = 0): 2M + 5S
+template <class F> LCV_FN void jac_dbl(jac<F>& r, const jac<F>& p) {
+  F A, B, C, D, E, G, t, x3, y3, z3;
+  f_sqr(A, p.x);
+  f_sqr(B, p.y);
+  f_sqr(C, B);
+  f_add(t, p.x, B);
+  f_sqr(t, t);
+  f_sub(t, t, A);
+  f_sub(t, t, C);
+  f_dbl(D, t);
+  f_dbl(E, A);
+  f_add(E, E, A);
+  f_sqr(G, E);
+  f_mul(z3, p.y, p.z);
+  f_dbl(z3, z3);
+  f_dbl(t, D);
+  f_sub(x3, G, t);
+  f_sub(t, D, x3);
+  f_mul(y3, E, t);
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_dbl(C, C);
+  f_sub(y3, y3, C);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+}
+
+// madd-2007-bl: p Jacobian, q affine (never the identity)
+template <class F> LCV_FN void jac_madd(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+  F z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
+  f_sqr(z1z1, p.z);
+  f_mul(u2, q.x, z1z1);
+  f_mul(s2, q.y, p.z);
+  f_mul(s2, s2, z1z1);
+  f_sub(h, u2, p.x);
+  f_sqr(hh, h);
+  f_dbl(i, hh);
+  f_dbl(i, i);
+  f_mul(j, h, i);
+  f_sub(rr, s2, p.y);
+  f_dbl(rr, rr);
+  f_mul(v, p.x, i);
+  f_sqr(x3, rr);
+  f_sub(x3, x3, j);
+  f_dbl(t, v);
+  f_sub(x3, x3, t);
+  f_sub(t, v, x3);
+  f_mul(y3, rr, t);
+  f_mul(t, p.y, j);
+  f_dbl(t, t);
+  f_sub(y3, y3, t);
+  f_add(z3, p.z, h);
+  f_sqr(z3, z3);
+  f_sub(z3, z3, z1z1);
+  f_sub(z3, z3, hh);
+  const bool pinf = f_is_zero(p.z);
+  const bool h0 = f_is_zero(h);
+  const bool r0 = f_is_zero(rr);
+  jac<F> res;
+  res.x = x3;
+  res.y = y3;
+  res.z = z3;
+  if (h0 && !pinf) {  // same x: doubling or P + (-P)
+    if (r0) {
+      jac<F> qq;
+      jac_from_aff(qq, q);
+      jac_dbl(res, qq);
+    } else {
+      jac_set_inf(res);
+    }
+  }
+  if (pinf) jac_from_aff(res, q);
+  r = res;
+}
+
+// add-2007-bl with complete case handling
+template <class F> LCV_FN void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+  F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t, x3, y3, z3;
+  f_sqr(z1z1, p.z);
+  f_sqr(z2z2, q.z);
+  f_mul(u1, p.x, z2z2);
+  f_mul(u2, q.x, z1z1);
+  f_mul(s1, p.y, q.z);
+  f_mul(s1, s1, z2z2);
+  f_mul(s2, q.y, p.z);
+  f_mul(s2, s2, z1z1);
+  f_sub(h, u2, u1);
+  f_dbl(i, h);
+  f_sqr(i, i);
+  f_mul(j, h, i);
+  f_sub(rr, s2, s1);
+  f_dbl(rr, rr);
+  f_mul(v, u1, i);
+  f_sqr(x3, rr);
+  f_sub(x3, x3, j);
+  f_dbl(t, v);
+  f_sub(x3, x3, t);
+  f_sub(t, v, x3);
+  f_mul(y3, rr, t);
+  f_mul(t, s1, j);
+  f_dbl(t, t);
+  f_sub(y3, y3, t);
+  f_add(z3, p.z, q.z);
+  f_sqr(z3, z3);
+  f_sub(z3, z3, z1z1);
+  f_sub(z3, z3, z2z2);
+  f_mul(z3, z3, h);
+  const bool pinf = f_is_zero(p.z);
+  const bool qinf = f_is_zero(q.z);
+  const bool h0 = f_is_zero(h);
+  const bool r0 = f_is_zero(rr);
+  jac<F> res;
+  res.x = x3;
+  res.y = y3;
+  res.z = z3;
+  if (h0 && !pinf && !qinf) {
+    if (r0) jac_dbl(res, p);
+    else jac_set_inf(res);
+  }
+  if (pinf) res = q;
+  if (qinf) res = p;
+  r = res;
+}
+
+template <class F> LCV_FN void jac_to_aff(aff<F>& r, const jac<F>& p) {
+  F zi, zi2;
+  f_inv(zi, p.z);
+  f_sqr(zi2, zi);
+  f_mul(r.x, p.x, zi2);
+  f_mul(zi2, zi2, zi);
+  f_mul(r.y, p.y, zi2);
+}
+
+// [|x|] P, x = -0xd201000000010000 (wave-uniform bit branch)
+template <class F> LCV_FN void jac_mul_xabs(jac<F>& r, const jac<F>& p) {
+  jac<F> acc = p;
+  LCV_NOUNROLL for (int i = 62; i >= 0; --i) {
+    jac_dbl(acc, acc);
+    if ((LCV_X_ABS >> i) & 1ull) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+template <class F> LCV_FN void jac_mul_xabs_aff(jac<F>& r, const aff<F>& p) {
+  jac<F> acc;
+  jac_from_aff(acc, p);
+  LCV_NOUNROLL for (int i = 62; i >= 0; --i) {
+    jac_dbl(acc, acc);
+    if ((LCV_X_ABS >> i) & 1ull) jac_madd(acc, acc, p);
+  }
+  r = acc;
+}
+// [x] P (x negative)
+template <class F> LCV_FN void jac_mul_x(jac<F>& r, const jac<F>& p) {
+  jac_mul_xabs(r, p);
+  jac_neg(r, r);
+}
+
+// variable 256-bit scalar (big-endian 32 bytes in global memory), double-and-add
+template <class F> LCV_FN void jac_mul_scalar_be32(jac<F>& r, const aff<F>& p, const uint8_t* k_be) {
+  jac<F> acc;
+  jac_set_inf(acc);
+  LCV_NOUNROLL for (int byte = 0; byte < 32; ++byte) {
+    const uint32_t kb = k_be[byte];
+    LCV_NOUNROLL for (int bit = 7; bit >= 0; --bit) {
+      jac_dbl(acc, acc);
+      jac<F> t;
+      jac_madd(t, acc, p);
+      if ((kb >> bit) & 1u) acc = t;
+    }
+  }
+  r = acc;
+}
+
+// ============================================================================ G1
+LCV_FN void g1_generator(g1a& r) { LCV_FP_SET(r.x, LCV_G1X_INIT); LCV_FP_SET(r.y, LCV_G1Y_INIT); }
+LCV_FN void g1_neg_generator(g1a& r) { LCV_FP_SET(r.x, LCV_G1X_INIT); LCV_FP_SET(r.y, LCV_G1NEGY_INIT); }
+
+enum { PT_OK = 0, PT_INF = 1, PT_BAD = 2 };
+
+// py_ecc decompress_G1 rules
+LCV_FN int g1_decompress(g1a& r, const uint8_t* in) {
+  const uint32_t b0 = in[0];
+  const uint32_t cflag = (b0 >> 7) & 1u, bflag = (b0 >> 6) & 1u, aflag = (b0 >> 5) & 1u;
+  fp xr;
+  fp_raw_from_be48(xr, in);
+  xr.v[11] &= 0x1fffffffu;
+  const uint32_t xz = fp_is_zero(xr) ? 1u : 0u;
+  if (!cflag || bflag != xz) return PT_BAD;
+  if (xz) return aflag ? PT_BAD : PT_INF;
+  if (!fp_raw_lt_p(xr)) return PT_BAD;
+  fp x, g, y, chk, four;
+  fp_to_mont(x, xr);
+  fp_sqr(g, x);
+  fp_mul(g, g, x);
+  LCV_FP_SET(four, LCV_FOUR_INIT);
+  fp_add(g, g, four);
+  fp_pow_p1d4(y, g);
+  fp_sqr(chk, y);
+  if (!fp_eq(chk, g)) return PT_BAD;
+  if (fp_is_large(y) != (aflag != 0)) fp_neg(y, y);
+  r.x = x;
+  r.y = y;
+  return PT_OK;
+}
+
+LCV_FN void g1_compress(uint8_t* out, const g1a& p, bool inf) {
+  if (inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 48; ++i) out[i] = 0;
+    return;
+  }
+  fp_to_be48(out, p.x);
+  out[0] |= 0x80 | (fp_is_large(p.y) ? 0x20 : 0);
+}
+
+// r * P == O  (definitional subgroup check; used once per committee key)
+LCV_FN bool g1_in_subgroup(const g1a& p) {
+  g1j acc;
+  jac_from_aff(acc, p);
+  LCV_NOUNROLL for (int i = LCV_R_SCALAR_BITS - 2; i >= 0; --i) {
+    jac_dbl(acc, acc);
+    if ((LCV_R_SCALAR[i >> 5] >> (i & 31)) & 1u) jac_madd(acc, acc, p);
+  }
+  return jac_is_inf(acc);
+}
+
+// ============================================================================ G2
+LCV_FN void g2_generator(g2a& r) { LCV_FP2_SET(r.x, LCV_G2X); LCV_FP2_SET(r.y, LCV_G2Y); }
+
+LCV_FN int g2_decompress(g2a& r, const uint8_t* in) {
+  const uint32_t b0 = in[0];
+  const uint32_t cflag = (b0 >> 7) & 1u, bflag = (b0 >> 6) & 1u, aflag = (b0 >> 5) & 1u;
+  fp x1r, x0r;
+  fp_raw_from_be48(x1r, in);
+  x1r.v[11] &= 0x1fffffffu;
+  fp_raw_from_be48(x0r, in + 48);
+  const uint32_t xz = (fp_is_zero(x1r) && fp_is_zero(x0r)) ? 1u : 0u;
+  if (!cflag || bflag != xz) return PT_BAD;
+  if (xz) return aflag ? PT_BAD : PT_INF;
+  if (!fp_raw_lt_p(x1r) || !fp_raw_lt_p(x0r)) return PT_BAD;
+  fp2 x, g, y, b;
+  fp_to_mont(x.c0, x0r);
+  fp_to_mont(x.c1, x1r);
+  fp2_sqr(g, x);
+  fp2_mul(g, g, x);
+  LCV_FP2_SET(b, LCV_B2);
+  fp2_add(g, g, b);
+  if (!fp2_sqrt(y, g)) return PT_BAD;
+  const bool large = fp_is_zero(y.c1) ? fp_is_large(y.c0) : fp_is_large(y.c1);
+  if (large != (aflag != 0)) fp2_neg(y, y);
+  r.x = x;
+  r.y = y;
+  return PT_OK;
+}
+
+LCV_FN void g2_compress(uint8_t* out, const g2a& p, bool inf) {
+  if (inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) out[i] = 0;
+    return;
+  }
+  fp_to_be48(out, p.x.c1);
+  fp_to_be48(out + 48, p.x.c0);
+  const bool large = fp_is_zero(p.y.c1) ? fp_is_large(p.y.c0) : fp_is_large(p.y.c1);
+  out[0] |= 0x80 | (large ? 0x20 : 0);
+}
+
+// psi(x, y) = (conj(x) cx, conj(y) cy), lifted to Jacobian coordinates
+LCV_FN void g2_psi(g2j& r, const g2j& p) {
+  fp2 cx, cy;
+  LCV_FP2_SET(cx, LCV_PSI_CX);
+  LCV_FP2_SET(cy, LCV_PSI_CY);
+  fp2_conj(r.x, p.x);
+  fp2_mul(r.x, r.x, cx);
+  fp2_conj(r.y, p.y);
+  fp2_mul(r.y, r.y, cy);
+  fp2_conj(r.z, p.z);
+}
+
+// Scott's test: P in G2  <=>  psi(P) == [x] P  (cross-checked against r*P in the oracle tests)
+LCV_FN bool g2_in_subgroup(const g2a& p) {
+  g2j t;
+  jac_mul_xabs_aff(t, p);  // [|x|]P ; [x]P = -t
+  if (jac_is_inf(t)) return false;
+  fp2 cx, cy, px, py, z2, z3, a, b;
+  LCV_FP2_SET(cx, LCV_PSI_CX);
+  LCV_FP2_SET(cy, LCV_PSI_CY);
+  fp2_conj(px, p.x);
+  fp2_mul(px, px, cx);
+  fp2_conj(py, p.y);
+  fp2_mul(py, py, cy);
+  fp2_sqr(z2, t.z);
+  fp2_mul(z3, z2, t.z);
+  fp2_mul(a, px, z2);
+  fp2_mul(b, py, z3);
+  fp2_neg(b, b);
+  return fp2_eq(a, t.x) && fp2_eq(b, t.y);
+}
+
+// RFC 9380 Appendix G.3: h_eff * P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)
+LCV_FN void g2_clear_cofactor(g2j& r, const g2j& p) {
+  g2j t1, t2, t3, u;
+  jac_mul_x(t1, p);   // t1 = c1 P
+  g2_psi(t2, p);      // t2 = psi(P)
+  jac_dbl(t3, p);     // t3 = 2P
+  g2_psi(t3, t3);
+  g2_psi(t3, t3);     // t3 = psi^2(2P)
+  jac_neg(u, t2);
+  jac_add(t3, t3, u); // t3 = t3 - t2
+  jac_add(t2, t1, t2);// t2 = t1 + t2
+  jac_mul_x(t2, t2);  // t2 = c1 t2
+  jac_add(t3, t3, t2);// t3 = t3 + t2
+  jac_neg(u, t1);
+  jac_add(t3, t3, u); // t3 = t3 - t1
+  jac_neg(u, p);
+  jac_add(r, t3, u);  // Q = t3 - P
+}
+
+}  // namespace lcv

@@ -1,0 +1,333 @@
+// lcv_field.hpp — BLS12-381 base field Fp and its quadratic extension Fp2 = Fp[u]/(u^2+1).
+//
+// Representation: 12 x 32-bit little-endian limbs, Montgomery form with R = 2^384, always fully
+// reduced into [0, p).  Multiplication is CIOS Montgomery with the "no-carry" shortcut (valid
+// because the top limb of p, 0x1a0111ea, is below 2^31 - 1): each 32x32+64 step maps to one
+// v_mad_u64_u32 on gfx950.  This is the arithmetic under `bls.FastAggregateVerify`
+// (reference call site sync-protocol.md:464; algorithm restated from the BLS12-381 standard,
+// see oracle/bls12_381.py for the CPU restatement the tests compare against).
+#pragma once
+#include "lcv_common.hpp"
+#include "lcv_consts.inc"
+
+namespace lcv {
+
+struct fp { uint32_t v[12]; };
+struct fp2 { fp c0, c1; };
+
+#define LCV_FP_SET(r, INIT) do { constexpr uint32_t _lcv_k[12] = INIT; LCV_UNROLL for (int _i = 0; _i < 12; ++_i) (r).v[_i] = _lcv_k[_i]; } while (0)
+#define LCV_FP2_SET(r, NAME) do { LCV_FP_SET((r).c0, NAME##_C0); LCV_FP_SET((r).c1, NAME##_C1); } while (0)
+
+LCV_FN void fp_zero(fp& r) { LCV_UNROLL for (int i = 0; i < 12; ++i) r.v[i] = 0; }
+LCV_FN void fp_one(fp& r) { LCV_FP_SET(r, LCV_ONE_INIT); }
+LCV_FN bool fp_is_zero(const fp& a) {
+  uint32_t x = 0;
+  LCV_UNROLL for (int i = 0; i < 12; ++i) x |= a.v[i];
+  return x == 0;
+}
+LCV_FN bool fp_eq(const fp& a, const fp& b) {
+  uint32_t x = 0;
+  LCV_UNROLL for (int i = 0; i < 12; ++i) x |= a.v[i] ^ b.v[i];
+  return x == 0;
+}
+LCV_FN void fp_sel(fp& r, bool c, const fp& a, const fp& b) {  // r = c ? a : b
+  LCV_UNROLL for (int i = 0; i < 12; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+}
+
+// t (< 2p) -> t mod p
+LCV_FN void fp_reduce_once(uint32_t r[12], const uint32_t t[12]) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint32_t d[12];
+  uint32_t br = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t s = (uint64_t)t[j] - PL[j] - br;
+    d[j] = (uint32_t)s;
+    br = (uint32_t)(s >> 63);
+  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) r[j] = br ? t[j] : d[j];
+}
+
+LCV_FN void fp_add(fp& r, const fp& a, const fp& b) {
+  uint32_t s[12];
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t x = (uint64_t)a.v[j] + b.v[j] + c;
+    s[j] = (uint32_t)x;
+    c = (uint32_t)(x >> 32);
+  }
+  fp_reduce_once(r.v, s);
+}
+
+LCV_FN void fp_sub(fp& r, const fp& a, const fp& b) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint32_t d[12];
+  uint32_t br = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t x = (uint64_t)a.v[j] - b.v[j] - br;
+    d[j] = (uint32_t)x;
+    br = (uint32_t)(x >> 63);
+  }
+  const uint32_t m = 0u - br;
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t x = (uint64_t)d[j] + (PL[j] & m) + c;
+    r.v[j] = (uint32_t)x;
+    c = (uint32_t)(x >> 32);
+  }
+}
+
+LCV_FN void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
+LCV_FN void fp_neg(fp& r, const fp& a) {
+  fp z;
+  fp_zero(z);
+  fp_sub(r, z, a);
+}
+LCV_FN void fp_half(fp& r, const fp& a) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  const uint32_t m = 0u - (a.v[0] & 1u);
+  uint32_t t[12];
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t x = (uint64_t)a.v[j] + (PL[j] & m) + c;
+    t[j] = (uint32_t)x;
+    c = (uint32_t)(x >> 32);
+  }
+  LCV_UNROLL for (int j = 0; j < 11; ++j) r.v[j] = (t[j] >> 1) | (t[j + 1] << 31);
+  r.v[11] = t[11] >> 1;
+}
+
+// CIOS Montgomery multiplication, no-carry variant.  r may alias a or b.
+LCV_FN void fp_mul_impl(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint32_t t[12];
+  LCV_UNROLL for (int j = 0; j < 12; ++j) t[j] = 0;
+  LCV_UNROLL for (int i = 0; i < 12; ++i) {
+    const uint32_t bi = b[i];
+    uint64_t c = (uint64_t)a[0] * bi + t[0];
+    uint32_t A = (uint32_t)(c >> 32);
+    const uint32_t m = (uint32_t)c * LCV_NP0;
+    uint64_t c2 = (uint64_t)m * PL[0] + (uint32_t)c;
+    uint32_t C = (uint32_t)(c2 >> 32);
+    LCV_UNROLL for (int j = 1; j < 12; ++j) {
+      c = (uint64_t)a[j] * bi + t[j] + A;
+      A = (uint32_t)(c >> 32);
+      c2 = (uint64_t)m * PL[j] + (uint32_t)c + C;
+      C = (uint32_t)(c2 >> 32);
+      t[j - 1] = (uint32_t)c2;
+    }
+    t[11] = A + C;
+  }
+  fp_reduce_once(r, t);
+}
+
+#if LCV_FP_CALL && !defined(LCV_HOSTSIM)
+struct fp_ret { uint32_t v[12]; };
+// Limbs travel as 24 scalar VGPR arguments / 12 returned VGPRs (clang's AMDGPU ABI passes
+// aggregates > 16 registers through the stack, scalars in v0..v31).
+__device__ __noinline__ fp_ret fp_mul_call(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
+                                           uint32_t a5, uint32_t a6, uint32_t a7, uint32_t a8, uint32_t a9,
+                                           uint32_t a10, uint32_t a11, uint32_t b0, uint32_t b1, uint32_t b2,
+                                           uint32_t b3, uint32_t b4, uint32_t b5, uint32_t b6, uint32_t b7,
+                                           uint32_t b8, uint32_t b9, uint32_t b10, uint32_t b11) {
+  const uint32_t a[12] = {a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11};
+  const uint32_t b[12] = {b0, b1, b2, b3, b4, b5, b6, b7, b8, b9, b10, b11};
+  fp_ret r;
+  fp_mul_impl(r.v, a, b);
+  return r;
+}
+LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
+  fp_ret x = fp_mul_call(a.v[0], a.v[1], a.v[2], a.v[3], a.v[4], a.v[5], a.v[6], a.v[7], a.v[8], a.v[9], a.v[10],
+                         a.v[11], b.v[0], b.v[1], b.v[2], b.v[3], b.v[4], b.v[5], b.v[6], b.v[7], b.v[8], b.v[9],
+                         b.v[10], b.v[11]);
+  LCV_COPY12(r.v, x.v);
+}
+#else
+LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) { fp_mul_impl(r.v, a.v, b.v); }
+#endif
+
+LCV_FN void fp_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }
+
+// Exponentiation by a fixed public exponent held in constant memory (wave-uniform branch).
+#define LCV_DEF_POW(fname, EXPARR, NBITS)                                  \
+  LCV_FN void fname(fp& r, const fp& a) {                                  \
+    fp acc = a;                                                            \
+    LCV_NOUNROLL for (int i = (NBITS) - 2; i >= 0; --i) {                  \
+      fp_sqr(acc, acc);                                                    \
+      if ((EXPARR[i >> 5] >> (i & 31)) & 1u) fp_mul(acc, acc, a);          \
+    }                                                                      \
+    r = acc;                                                               \
+  }
+LCV_DEF_POW(fp_inv, LCV_EXP_P_MINUS_2, LCV_EXP_P_MINUS_2_BITS)           // a^(p-2) (inv0: 0 -> 0)
+LCV_DEF_POW(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
+LCV_DEF_POW(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
+LCV_DEF_POW(fp_pow_pm1d2, LCV_EXP_P_MINUS_1_DIV_2, LCV_EXP_P_MINUS_1_DIV_2_BITS)  // Legendre
+
+// ---- conversions (raw = canonical integer limbs, not Montgomery)
+LCV_FN void fp_to_mont(fp& r, const fp& raw) {
+  fp r2;
+  LCV_FP_SET(r2, LCV_R2_INIT);
+  fp_mul(r, raw, r2);
+}
+LCV_FN void fp_from_mont(fp& raw, const fp& a) {
+  fp one;
+  fp_zero(one);
+  one.v[0] = 1;
+  fp_mul(raw, a, one);
+}
+LCV_FN void fp_raw_from_be48(fp& r, const uint8_t* p) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) r.v[k] = ld_be32(p + 44 - 4 * k);
+}
+LCV_FN void fp_raw_to_be48(uint8_t* p, const fp& r) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) st_be32(p + 44 - 4 * k, r.v[k]);
+}
+// a < b on raw limbs
+LCV_FN bool fp_raw_lt(const fp& a, const fp& b) {
+  uint32_t br = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t s = (uint64_t)a.v[j] - b.v[j] - br;
+    br = (uint32_t)(s >> 63);
+  }
+  return br != 0;
+}
+LCV_FN bool fp_raw_lt_p(const fp& a) {
+  fp p;
+  LCV_FP_SET(p, LCV_P_INIT);
+  return fp_raw_lt(a, p);
+}
+// "lexicographically largest": canonical value > (p-1)/2
+LCV_FN bool fp_is_large(const fp& a_mont) {
+  fp raw, half;
+  fp_from_mont(raw, a_mont);
+  LCV_FP_SET(half, LCV_HALF_P_RAW_INIT);
+  return fp_raw_lt(half, raw);
+}
+LCV_FN void fp_to_be48(uint8_t* p, const fp& a_mont) {
+  fp raw;
+  fp_from_mont(raw, a_mont);
+  fp_raw_to_be48(p, raw);
+}
+LCV_FN void fp_from_be48_mont(fp& r, const uint8_t* p) {  // caller guarantees value < p
+  fp raw;
+  fp_raw_from_be48(raw, p);
+  fp_to_mont(r, raw);
+}
+
+// ============================================================================ Fp2
+LCV_FN void fp2_zero(fp2& r) { fp_zero(r.c0); fp_zero(r.c1); }
+LCV_FN void fp2_one(fp2& r) { fp_one(r.c0); fp_zero(r.c1); }
+LCV_FN bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+LCV_FN bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+LCV_FN void fp2_sel(fp2& r, bool c, const fp2& a, const fp2& b) { fp_sel(r.c0, c, a.c0, b.c0); fp_sel(r.c1, c, a.c1, b.c1); }
+LCV_FN void fp2_add(fp2& r, const fp2& a, const fp2& b) { fp_add(r.c0, a.c0, b.c0); fp_add(r.c1, a.c1, b.c1); }
+LCV_FN void fp2_sub(fp2& r, const fp2& a, const fp2& b) { fp_sub(r.c0, a.c0, b.c0); fp_sub(r.c1, a.c1, b.c1); }
+LCV_FN void fp2_dbl(fp2& r, const fp2& a) { fp_dbl(r.c0, a.c0); fp_dbl(r.c1, a.c1); }
+LCV_FN void fp2_neg(fp2& r, const fp2& a) { fp_neg(r.c0, a.c0); fp_neg(r.c1, a.c1); }
+LCV_FN void fp2_half(fp2& r, const fp2& a) { fp_half(r.c0, a.c0); fp_half(r.c1, a.c1); }
+LCV_FN void fp2_conj(fp2& r, const fp2& a) { r.c0 = a.c0; fp_neg(r.c1, a.c1); }
+LCV_FN void fp2_mul_fp(fp2& r, const fp2& a, const fp& s) { fp_mul(r.c0, a.c0, s); fp_mul(r.c1, a.c1, s); }
+
+// Karatsuba: 3 Fp multiplications.  r may alias a or b.
+LCV_FN void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
+  fp t0, t1, t2, t3;
+  fp_mul(t0, a.c0, b.c0);
+  fp_mul(t1, a.c1, b.c1);
+  fp_add(t2, a.c0, a.c1);
+  fp_add(t3, b.c0, b.c1);
+  fp_mul(t2, t2, t3);
+  fp_sub(r.c0, t0, t1);
+  fp_sub(t2, t2, t0);
+  fp_sub(r.c1, t2, t1);
+}
+// (a0 + a1 u)^2 = (a0+a1)(a0-a1) + 2 a0 a1 u
+LCV_FN void fp2_sqr(fp2& r, const fp2& a) {
+  fp t0, t1, t2;
+  fp_add(t0, a.c0, a.c1);
+  fp_sub(t1, a.c0, a.c1);
+  fp_mul(t2, a.c0, a.c1);
+  fp_mul(r.c0, t0, t1);
+  fp_dbl(r.c1, t2);
+}
+// multiply by xi = 1 + u
+LCV_FN void fp2_mul_xi(fp2& r, const fp2& a) {
+  fp t;
+  fp_sub(t, a.c0, a.c1);
+  fp_add(r.c1, a.c0, a.c1);
+  r.c0 = t;
+}
+LCV_FN void fp2_inv(fp2& r, const fp2& a) {
+  fp t0, t1;
+  fp_sqr(t0, a.c0);
+  fp_sqr(t1, a.c1);
+  fp_add(t0, t0, t1);
+  fp_inv(t1, t0);
+  fp_mul(r.c0, a.c0, t1);
+  fp_mul(t0, a.c1, t1);
+  fp_neg(r.c1, t0);
+}
+LCV_FN void fp2_norm(fp& n, const fp2& a) {
+  fp t;
+  fp_sqr(n, a.c0);
+  fp_sqr(t, a.c1);
+  fp_add(n, n, t);
+}
+
+// Square root given alpha = norm(a)^((p+1)/4) (so alpha^2 == norm(a) iff a is a square).
+// Two-exponentiation method: delta = (a0 + alpha)/2, t = delta^((p-3)/4), c = t*delta,
+// s = t^2 delta = +-1; then sqrt(a) = (c, a1 t/2) if s == 1 else (-a1 t/2, c).
+// a1 == 0 is handled by the same exponentiation on delta = a0.  Returns y^2 == a.
+LCV_FN bool fp2_sqrt_alpha(fp2& y, const fp2& a, const fp& alpha) {
+  const bool a1z = fp_is_zero(a.c1);
+  fp delta;
+  fp_add(delta, a.c0, alpha);
+  fp_half(delta, delta);
+  fp_sel(delta, a1z, a.c0, delta);
+  fp t, c, s;
+  fp_pow_p3d4(t, delta);
+  fp_mul(c, t, delta);
+  fp_mul(s, c, t);
+  fp one;
+  fp_one(one);
+  const bool s_one = fp_eq(s, one);
+  fp u, nu;
+  fp_half(u, a.c1);
+  fp_mul(u, u, t);
+  fp_neg(nu, u);
+  fp zero;
+  fp_zero(zero);
+  // a1 == 0: (c, 0) if s==1 or delta==0 else (0, c); general: (c, u) if s==1 else (-u, c)
+  const bool first = a1z ? (s_one || fp_is_zero(delta)) : s_one;
+  fp y0a, y1a;
+  fp_sel(y0a, a1z, zero, nu);      // second-form real part
+  fp_sel(y1a, a1z, zero, u);       // first-form imaginary part
+  fp_sel(y.c0, first, c, y0a);
+  fp_sel(y.c1, first, y1a, c);
+  fp2 chk;
+  fp2_sqr(chk, y);
+  return fp2_eq(chk, a);
+}
+LCV_FN bool fp2_sqrt(fp2& y, const fp2& a) {
+  fp n, alpha;
+  fp2_norm(n, a);
+  fp_pow_p1d4(alpha, n);
+  return fp2_sqrt_alpha(y, a, alpha);
+}
+// is_square(a) via the norm; also returns alpha for reuse by fp2_sqrt_alpha
+LCV_FN bool fp2_is_square_alpha(const fp2& a, fp& alpha) {
+  fp n, chk;
+  fp2_norm(n, a);
+  fp_pow_p1d4(alpha, n);
+  fp_sqr(chk, alpha);
+  return fp_eq(chk, n);
+}
+// RFC 9380 sgn0 for m = 2 (on canonical values)
+LCV_FN uint32_t fp2_sgn0(const fp2& a) {
+  fp r0, r1;
+  fp_from_mont(r0, a.c0);
+  fp_from_mont(r1, a.c1);
+  const uint32_t sign0 = r0.v[0] & 1u;
+  const uint32_t zero0 = fp_is_zero(r0) ? 1u : 0u;
+  const uint32_t sign1 = r1.v[0] & 1u;
+  return sign0 | (zero0 & sign1);
+}
+
+}  // namespace lcv

@@ -1,0 +1,77 @@
+// lcv_hostsim.cpp — TEST-ONLY host simulation of liblcv.so (built as liblcv_hostsim.so).
+// Runs the exact per-item device code of lcv_items.hpp in plain host loops (OpenMP), so the CPU-only
+// test suite can check the device arithmetic against the oracle.  The product package `lcv` never
+// loads this library; it exists only for tests/ (see DESIGN.md "Testing without a GPU").
+#define LCV_HOSTSIM 1
+#include <chrono>
+#include <new>
+#include <stdlib.h>
+#include <string>
+#include <vector>
+
+#define LCV_HD
+
+struct lcv_ctx;
+
+struct Backend {
+  int open_stage = -1;
+  std::chrono::steady_clock::time_point t0;
+};
+
+static int be_init(lcv_ctx* ctx, int device);
+static void be_destroy(lcv_ctx* ctx);
+static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes);
+static void be_free(lcv_ctx* ctx, void* p);
+static int be_h2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes);
+static int be_d2h(lcv_ctx* ctx, void* dst, const void* src, size_t bytes);
+static int be_d2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes);
+static int be_memset(lcv_ctx* ctx, void* p, int v, size_t bytes);
+static int be_sync(lcv_ctx* ctx);
+template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
+static void be_stage_begin(lcv_ctx* ctx, int stage);
+static void be_stage_end(lcv_ctx* ctx, int stage);
+static void be_reset_timings(lcv_ctx* ctx);
+static void be_collect_timings(lcv_ctx* ctx);
+
+#include "lcv_driver.inc"
+
+static int be_init(lcv_ctx* ctx, int device) {
+  if (device != 0) return fail(ctx, LCV_EDEVICE, "hostsim: only device 0");
+  return LCV_OK;
+}
+static void be_destroy(lcv_ctx*) {}
+static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
+  *p = calloc(1, bytes ? bytes : 1);
+  return *p ? LCV_OK : fail(ctx, LCV_ENOMEM, "hostsim: out of memory");
+}
+static void be_free(lcv_ctx*, void* p) { free(p); }
+static int be_h2d(lcv_ctx*, void* dst, const void* src, size_t bytes) { memcpy(dst, src, bytes); return LCV_OK; }
+static int be_d2h(lcv_ctx*, void* dst, const void* src, size_t bytes) { memcpy(dst, src, bytes); return LCV_OK; }
+static int be_d2d(lcv_ctx*, void* dst, const void* src, size_t bytes) { memmove(dst, src, bytes); return LCV_OK; }
+static int be_memset(lcv_ctx*, void* p, int v, size_t bytes) { memset(p, v, bytes); return LCV_OK; }
+static int be_sync(lcv_ctx*) { return LCV_OK; }
+template <class F> static int be_launch(lcv_ctx*, const F& f, uint32_t n) {
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t i = 0; i < (int64_t)n; ++i) f((uint32_t)i);
+  return LCV_OK;
+}
+static void be_stage_begin(lcv_ctx* ctx, int stage) {
+  ctx->be.open_stage = stage;
+  ctx->be.t0 = std::chrono::steady_clock::now();
+}
+static void be_stage_end(lcv_ctx* ctx, int stage) {
+  if (ctx->be.open_stage != stage) return;
+  const auto t1 = std::chrono::steady_clock::now();
+  ctx->stage_ms[stage] += std::chrono::duration<float, std::milli>(t1 - ctx->be.t0).count();
+  ctx->be.open_stage = -1;
+}
+static void be_reset_timings(lcv_ctx* ctx) {
+  for (int s = 0; s < ST_COUNT; ++s) ctx->stage_ms[s] = 0.f;
+}
+static void be_collect_timings(lcv_ctx*) {}
+
+extern "C" int lcv_device_count(int* out) {
+  if (!out) return LCV_EINVAL;
+  *out = 1;
+  return LCV_OK;
+}

@@ -1,0 +1,430 @@
+// lcv_items.hpp — per-item bodies of every stage of the batched verifier.  Each function processes
+// ONE item (an update, a committee key, a (update, pairing) pair ...) and is called by
+//   * the HIP kernels in lcv_hip.hip (one lane per item), and
+//   * the host-simulation test build lcv_hostsim.cpp (a plain loop), so the exact device
+//     arithmetic can be checked against the CPU oracle in the CPU-only test suite.
+// All intermediate device buffers are structure-of-arrays with stride `cap` (lane i of a wave reads
+// consecutive 32-bit words -> coalesced).
+//
+// Stage map onto the reference's validate_light_client_update (sync-protocol.md:386-465):
+//   item_nsc        hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449)
+//   item_pre        every non-BLS assert (:392-449) + signing root (:460-463) -> first failing reason
+//   item_h2c        hash_to_G2(signing_root)                   -+
+//   item_sig        signature decode + subgroup check           |  bls.FastAggregateVerify (:464)
+//   item_agg        masked G1 aggregation of participant keys   |
+//   item_lines / item_miller / item_final_exp   pairing check  -+
+//   item_verdict    conjunction + reason code
+#pragma once
+#include "lcv_h2c.hpp"
+#include "lcv_pairing.hpp"
+#include "lcv_ssz.hpp"
+
+namespace lcv {
+
+struct BatchDev {
+  const uint8_t* att_beacon;
+  const uint8_t* att_exec;
+  const uint8_t* att_branch;
+  const uint8_t* fin_beacon;
+  const uint8_t* fin_exec;
+  const uint8_t* fin_branch;
+  const uint8_t* nsc_pool;
+  const uint32_t* nsc_index;
+  const uint8_t* nsc_branch;
+  const uint8_t* finality_branch;
+  const uint8_t* bits;
+  const uint8_t* sig;
+  const uint64_t* sig_slot;
+  uint32_t n;
+  uint32_t npool;
+};
+
+struct Params {
+  uint64_t current_slot;
+  uint64_t store_fin_slot;
+  uint32_t next_known;
+  uint32_t gvr[8];  // big-endian words
+};
+
+struct CommitteeDev {
+  const uint8_t* next_raw;   // store.next_sync_committee SSZ bytes (24624)
+  uint32_t* pts;             // [ncomm][512][24]  affine x,y (Montgomery)
+  uint32_t* sum_all;         // [ncomm][36]       Jacobian sum of all valid keys
+  uint32_t* badmask;         // [ncomm][16]       invalid-key bitmap
+  uint8_t* key_status;       // [ncomm][512]      PT_OK, or PT_BAD (undecodable / identity / not in G1)
+  const uint8_t* raw;        // [ncomm][raw_stride] compressed pubkeys, key j at +48 j
+  uint32_t raw_stride;       // 24624 for SSZ SyncCommittee, 24576 for bare key tables
+  uint32_t ncomm;
+};
+
+struct Work {
+  uint32_t cap;
+  uint32_t pool_cap;
+  uint32_t* msg;         // [8][cap]
+  uint8_t* pre_reason;   // [cap]
+  uint32_t* comm_id;     // [cap] committee used for the signature (0 current, 1 next)
+  uint32_t* nsc_root;    // [8][pool_cap]
+  uint8_t* nsc_flags;    // [pool_cap] bit0: all-zero, bit1: equals store.next_sync_committee
+  uint32_t* qh;          // [48][cap] H(m) affine (x0,x1,y0,y1)
+  uint8_t* qh_inf;       // [cap]
+  uint32_t* qs;          // [48][cap] signature affine
+  uint8_t* sig_status;   // [cap]
+  uint32_t* pk;          // [24][cap] aggregate pubkey affine
+  uint8_t* agg_status;   // [cap]
+  uint32_t* lines;       // [2][68][72][cap]
+  uint32_t* f;           // [144][cap]
+  uint8_t* pair_ok;      // [cap]
+  uint8_t* verdict;      // [cap]
+  uint8_t* reason;       // [cap]
+};
+
+// ---- SoA helpers
+LCV_FN void soa_ld_fp(fp& r, const uint32_t* base, size_t cap, size_t i, size_t slot) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) r.v[k] = base[(slot * 12 + k) * cap + i];
+}
+LCV_FN void soa_st_fp(uint32_t* base, size_t cap, size_t i, size_t slot, const fp& a) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) base[(slot * 12 + k) * cap + i] = a.v[k];
+}
+LCV_FN void soa_ld_fp2(fp2& r, const uint32_t* base, size_t cap, size_t i, size_t slot) {
+  soa_ld_fp(r.c0, base, cap, i, 2 * slot);
+  soa_ld_fp(r.c1, base, cap, i, 2 * slot + 1);
+}
+LCV_FN void soa_st_fp2(uint32_t* base, size_t cap, size_t i, size_t slot, const fp2& a) {
+  soa_st_fp(base, cap, i, 2 * slot, a.c0);
+  soa_st_fp(base, cap, i, 2 * slot + 1, a.c1);
+}
+LCV_FN void soa_ld_fp12(fp12& r, const uint32_t* base, size_t cap, size_t i) {
+  soa_ld_fp2(r.c0.c0, base, cap, i, 0); soa_ld_fp2(r.c0.c1, base, cap, i, 1); soa_ld_fp2(r.c0.c2, base, cap, i, 2);
+  soa_ld_fp2(r.c1.c0, base, cap, i, 3); soa_ld_fp2(r.c1.c1, base, cap, i, 4); soa_ld_fp2(r.c1.c2, base, cap, i, 5);
+}
+LCV_FN void soa_st_fp12(uint32_t* base, size_t cap, size_t i, const fp12& a) {
+  soa_st_fp2(base, cap, i, 0, a.c0.c0); soa_st_fp2(base, cap, i, 1, a.c0.c1); soa_st_fp2(base, cap, i, 2, a.c0.c2);
+  soa_st_fp2(base, cap, i, 3, a.c1.c0); soa_st_fp2(base, cap, i, 4, a.c1.c1); soa_st_fp2(base, cap, i, 5, a.c1.c2);
+}
+LCV_FN void soa_ld_h256(h256& r, const uint32_t* base, size_t cap, size_t i) {
+  LCV_UNROLL for (int k = 0; k < 8; ++k) r.w[k] = base[k * cap + i];
+}
+LCV_FN void soa_st_h256(uint32_t* base, size_t cap, size_t i, const h256& a) {
+  LCV_UNROLL for (int k = 0; k < 8; ++k) base[k * cap + i] = a.w[k];
+}
+
+// ============================================================================ SSZ stage
+LCV_FN void item_nsc(uint32_t j, const BatchDev& B, const CommitteeDev& C, const Params& P, const Work& W) {
+  const uint8_t* sc = B.nsc_pool + (size_t)K_SC * j;
+  h256 root;
+  htr_sync_committee(root, sc);
+  soa_st_h256(W.nsc_root, W.pool_cap, j, root);
+  const uint32_t* a = (const uint32_t*)sc;
+  const uint32_t* b = (const uint32_t*)C.next_raw;
+  uint32_t orz = 0, dif = 0;
+  for (int k = 0; k < K_SC / 4; ++k) {
+    const uint32_t x = a[k];
+    orz |= x;
+    dif |= x ^ b[k];
+  }
+  W.nsc_flags[j] = (uint8_t)((orz == 0 ? 1u : 0u) | (dif == 0 ? 2u : 0u));
+}
+
+LCV_FN uint32_t popcount_bits(const uint8_t* bits) {
+  uint32_t pc = 0;
+  LCV_UNROLL for (int w = 0; w < 16; ++w) pc += (uint32_t)__builtin_popcount(((const uint32_t*)bits)[w]);
+  return pc;
+}
+
+LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const Params& P, const Work& W) {
+  (void)C;
+  const uint8_t* ab = B.att_beacon + (size_t)K_BEACON * i;
+  const uint8_t* ae = B.att_exec + (size_t)K_EXEC * i;
+  const uint8_t* abr = B.att_branch + (size_t)K_EXEC_BRANCH * i;
+  const uint8_t* fb = B.fin_beacon + (size_t)K_BEACON * i;
+  const uint8_t* fe = B.fin_exec + (size_t)K_EXEC * i;
+  const uint8_t* fbr = B.fin_branch + (size_t)K_EXEC_BRANCH * i;
+  const uint8_t* nbr = B.nsc_branch + (size_t)K_NSC_BRANCH * i;
+  const uint8_t* finb = B.finality_branch + (size_t)K_FIN_BRANCH * i;
+  const uint32_t pool = B.nsc_index[i];
+  const uint64_t sig_slot = B.sig_slot[i];
+  const uint64_t att_slot = ld_le64(ab);
+  const uint64_t fin_slot = ld_le64(fb);
+  uint32_t reason = 0;
+#define LCV_FAIL(k) do { if (reason == 0) reason = (k); } while (0)
+  // :392 participants
+  if (popcount_bits(B.bits + 64 * (size_t)i) < 1) LCV_FAIL(1);
+  // :395 attested header
+  if (!lc_header_valid(ab, ae, abr)) LCV_FAIL(2);
+  // :398 slot ordering
+  if (!(P.current_slot >= sig_slot && sig_slot > att_slot && att_slot >= fin_slot)) LCV_FAIL(3);
+  const uint64_t store_period = period_of_slot(P.store_fin_slot);
+  const uint64_t sig_period = period_of_slot(sig_slot);
+  const bool next_known = P.next_known != 0;
+  if (next_known) {
+    if (!(sig_period == store_period || sig_period == store_period + 1)) LCV_FAIL(4);  // :402
+  } else {
+    if (sig_period != store_period) LCV_FAIL(5);  // :404
+  }
+  // :407-414 relevance
+  const uint64_t att_period = period_of_slot(att_slot);
+  const bool is_sc = !bytes_all_zero(nbr, K_NSC_BRANCH / 4);
+  const bool has_next = !next_known && is_sc && att_period == store_period;
+  if (!(att_slot > P.store_fin_slot || has_next)) LCV_FAIL(6);
+  // :419-434 finality
+  h256 state_root;
+  ld_chunk(state_root, ab + 48);
+  const bool is_fin = !bytes_all_zero(finb, K_FIN_BRANCH / 4);
+  const bool fin_default = bytes_all_zero(fb, K_BEACON / 4) && bytes_all_zero(fe, K_EXEC / 4) &&
+                           bytes_all_zero(fbr, K_EXEC_BRANCH / 4);
+  if (!is_fin) {
+    if (!fin_default) LCV_FAIL(7);
+  } else {
+    h256 leaf;
+    if (fin_slot == 0) {
+      if (!fin_default) LCV_FAIL(8);
+      h256_zero(leaf);
+    } else {
+      if (!lc_header_valid(fb, fe, fbr)) LCV_FAIL(9);
+      htr_beacon(leaf, fb);
+    }
+    if (!merkle_branch_ok(leaf, finb, 6, 41, state_root)) LCV_FAIL(10);
+  }
+  // :438-449 next sync committee
+  const uint32_t nflags = W.nsc_flags[pool];
+  if (!is_sc) {
+    if (!(nflags & 1u)) LCV_FAIL(11);
+  } else {
+    if (att_period == store_period && next_known && !(nflags & 2u)) LCV_FAIL(12);
+    h256 leaf;
+    soa_ld_h256(leaf, W.nsc_root, W.pool_cap, pool);
+    if (!merkle_branch_ok(leaf, nbr, 5, 23, state_root)) LCV_FAIL(13);
+  }
+#undef LCV_FAIL
+  // :452-463 committee selection and signing root
+  W.comm_id[i] = sig_period != store_period ? 1u : 0u;
+  h256 gvr, msg;
+  LCV_UNROLL for (int k = 0; k < 8; ++k) gvr.w[k] = P.gvr[k];
+  signing_root(msg, ab, sig_slot, gvr);
+  soa_st_h256(W.msg, W.cap, i, msg);
+  W.pre_reason[i] = (uint8_t)reason;
+}
+
+// ============================================================================ BLS stages
+LCV_FN void st_g2a(uint32_t* base, size_t cap, size_t i, const g2a& q) {
+  soa_st_fp2(base, cap, i, 0, q.x);
+  soa_st_fp2(base, cap, i, 1, q.y);
+}
+LCV_FN void ld_g2a(g2a& q, const uint32_t* base, size_t cap, size_t i) {
+  soa_ld_fp2(q.x, base, cap, i, 0);
+  soa_ld_fp2(q.y, base, cap, i, 1);
+}
+
+LCV_FN void item_h2c(uint32_t i, const Work& W) {
+  h256 msg;
+  soa_ld_h256(msg, W.msg, W.cap, i);
+  g2j q;
+  hash_to_g2(q, msg);
+  const bool inf = jac_is_inf(q);
+  g2a a;
+  jac_to_aff(a, q);
+  st_g2a(W.qh, W.cap, i, a);
+  W.qh_inf[i] = inf ? 1 : 0;
+}
+
+LCV_FN void item_sig(uint32_t i, const BatchDev& B, const Work& W) {
+  g2a s;
+  fp2_zero(s.x);
+  fp2_zero(s.y);
+  int st = g2_decompress(s, B.sig + 96 * (size_t)i);
+  if (st == PT_OK && !g2_in_subgroup(s)) st = PT_BAD;
+  st_g2a(W.qs, W.cap, i, s);
+  W.sig_status[i] = (uint8_t)st;
+}
+
+LCV_FN void ld_g1a_tbl(g1a& p, const uint32_t* pts, size_t idx) {
+  const uint32_t* q = pts + idx * 24;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { p.x.v[k] = q[k]; p.y.v[k] = q[12 + k]; }
+}
+
+// masked aggregation of the selected committee (sync-protocol.md:452-459 + FastAggregateVerify's
+// aggregate).  Complement trick: with more than 256 participants, sum_all - sum(non-participants).
+LCV_FN void item_agg(uint32_t i, const BatchDev& B, const CommitteeDev& C, const Work& W) {
+  const uint32_t c = W.comm_id[i];
+  const uint32_t* bw = (const uint32_t*)(B.bits + 64 * (size_t)i);
+  const uint32_t* bad = C.badmask + 16 * c;
+  uint32_t pc = 0, anybad = 0;
+  LCV_UNROLL for (int w = 0; w < 16; ++w) {
+    pc += (uint32_t)__builtin_popcount(bw[w]);
+    anybad |= bw[w] & bad[w];
+  }
+  const bool comp = pc > 256;
+  g1j acc;
+  if (comp) {
+    const uint32_t* s = C.sum_all + 36 * c;
+    LCV_UNROLL for (int k = 0; k < 12; ++k) { acc.x.v[k] = s[k]; acc.y.v[k] = s[12 + k]; acc.z.v[k] = s[24 + k]; }
+  } else {
+    jac_set_inf(acc);
+  }
+  const uint32_t* pts = C.pts + (size_t)c * 512 * 24;
+  LCV_NOUNROLL for (int w = 0; w < 16; ++w) {
+    uint32_t m = comp ? (~bw[w] & ~bad[w]) : bw[w];
+    while (m) {
+      const int b = __builtin_ctz(m);
+      m &= m - 1;
+      g1a p;
+      ld_g1a_tbl(p, pts, 32 * w + b);
+      if (comp) fp_neg(p.y, p.y);
+      jac_madd(acc, acc, p);
+    }
+  }
+  const bool inf = jac_is_inf(acc);
+  g1a a;
+  jac_to_aff(a, acc);
+  soa_st_fp(W.pk, W.cap, i, 0, a.x);
+  soa_st_fp(W.pk, W.cap, i, 1, a.y);
+  W.agg_status[i] = (uint8_t)(anybad ? PT_BAD : (inf || pc == 0 ? PT_INF : PT_OK));
+}
+
+LCV_FN size_t line_slot(uint32_t k, uint32_t step, uint32_t e) { return ((size_t)k * LCV_MILLER_STEPS + step) * 6 + e; }
+
+LCV_FN void st_line(const Work& W, uint32_t i, uint32_t k, uint32_t step, const line3& L) {
+  soa_st_fp2(W.lines, W.cap, i, line_slot(k, step, 0) / 2, L.c00);
+  soa_st_fp2(W.lines, W.cap, i, line_slot(k, step, 2) / 2, L.c01);
+  soa_st_fp2(W.lines, W.cap, i, line_slot(k, step, 4) / 2, L.c11);
+}
+LCV_FN void ld_line(line3& L, const Work& W, uint32_t i, uint32_t k, uint32_t step) {
+  soa_ld_fp2(L.c00, W.lines, W.cap, i, line_slot(k, step, 0) / 2);
+  soa_ld_fp2(L.c01, W.lines, W.cap, i, line_slot(k, step, 2) / 2);
+  soa_ld_fp2(L.c11, W.lines, W.cap, i, line_slot(k, step, 4) / 2);
+}
+
+// t in [0, 2n): k = t / n selects the G2 point (0: H(m), 1: signature), i = t % n
+LCV_FN void item_lines(uint32_t t, uint32_t n, const Work& W) {
+  const uint32_t k = t / n, i = t % n;
+  g2a Q;
+  ld_g2a(Q, k == 0 ? W.qh : W.qs, W.cap, i);
+  const bool qinf = (k == 0) ? (W.qh_inf[i] != 0) : (W.sig_status[i] != PT_OK);
+  g2j T;
+  jac_from_aff(T, Q);
+  uint32_t step = 0;
+  LCV_NOUNROLL for (int b = 62; b >= 0; --b) {
+    line3 L;
+    line_dbl(T, L);
+    if (qinf) { fp2_one(L.c00); fp2_zero(L.c01); fp2_zero(L.c11); }
+    st_line(W, i, k, step++, L);
+    if ((LCV_X_ABS >> b) & 1ull) {
+      line_add(T, L, Q);
+      if (qinf) { fp2_one(L.c00); fp2_zero(L.c01); fp2_zero(L.c11); }
+      st_line(W, i, k, step++, L);
+    }
+  }
+}
+
+LCV_FN void item_miller(uint32_t i, const Work& W) {
+  fp nx0, y0, nx1, y1;
+  soa_ld_fp(nx0, W.pk, W.cap, i, 0);
+  fp_neg(nx0, nx0);
+  soa_ld_fp(y0, W.pk, W.cap, i, 1);
+  LCV_FP_SET(nx1, LCV_G1X_INIT);
+  fp_neg(nx1, nx1);
+  LCV_FP_SET(y1, LCV_G1NEGY_INIT);  // P2 = -G1
+  fp12 f;
+  fp12_one(f);
+  uint32_t step = 0;
+  LCV_NOUNROLL for (int b = 62; b >= 0; --b) {
+    line3 L;
+    fp12_sqr(f, f);
+    ld_line(L, W, i, 0, step);
+    fp12_apply_line(f, L, nx0, y0);
+    ld_line(L, W, i, 1, step);
+    fp12_apply_line(f, L, nx1, y1);
+    ++step;
+    if ((LCV_X_ABS >> b) & 1ull) {
+      ld_line(L, W, i, 0, step);
+      fp12_apply_line(f, L, nx0, y0);
+      ld_line(L, W, i, 1, step);
+      fp12_apply_line(f, L, nx1, y1);
+      ++step;
+    }
+  }
+  fp12_conj(f, f);  // x < 0
+  soa_st_fp12(W.f, W.cap, i, f);
+}
+
+// final exponentiation (result e^3, see lcv_pairing.hpp) and the "== 1" test
+LCV_FN void final_exp(fp12& r, const fp12& f) {
+  fp12 m, t0, t1, t2;
+  final_exp_easy(m, f);
+  fp12_exp_xabs(t0, m);
+  fp12_mul(t0, t0, m);
+  fp12_conj(t0, t0);            // A  = m^(x-1)
+  fp12_exp_xabs(t1, t0);
+  fp12_mul(t1, t1, t0);
+  fp12_conj(t1, t1);            // A2 = A^(x-1)
+  fp12_exp_xabs(t0, t1);
+  fp12_conj(t0, t0);
+  fp12_frob1(t1, t1);
+  fp12_mul(t0, t0, t1);         // B  = A2^(x+p)
+  fp12_exp_xabs(t1, t0);
+  fp12_exp_xabs(t1, t1);        // B^(x^2)
+  fp12_frob2(t2, t0);
+  fp12_mul(t1, t1, t2);
+  fp12_conj(t2, t0);
+  fp12_mul(t1, t1, t2);         // C  = B^(x^2 + p^2 - 1)
+  fp12_cyclotomic_sqr(t0, m);
+  fp12_mul(t0, t0, m);
+  fp12_mul(r, t1, t0);          // C * m^3
+}
+
+LCV_FN void item_final_exp(uint32_t i, const Work& W) {
+  fp12 f, r;
+  soa_ld_fp12(f, W.f, W.cap, i);
+  final_exp(r, f);
+  W.pair_ok[i] = fp12_is_one(r) ? 1 : 0;
+  soa_st_fp12(W.f, W.cap, i, r);  // keep the pairing value for the parity tests
+}
+
+LCV_FN void item_verdict(uint32_t i, const Work& W) {
+  uint32_t reason = W.pre_reason[i];
+  if (reason == 0) {
+    const bool ok = W.agg_status[i] == PT_OK && W.sig_status[i] != PT_BAD && W.pair_ok[i] != 0;
+    reason = ok ? 0 : 14;  // :464
+  }
+  W.reason[i] = (uint8_t)reason;
+  W.verdict[i] = reason == 0 ? 1 : 0;
+}
+
+// ============================================================================ committee setup
+LCV_FN void item_committee_key(uint32_t t, const CommitteeDev& C) {
+  const uint32_t c = t / 512, j = t % 512;
+  g1a p;
+  fp_zero(p.x);
+  fp_zero(p.y);
+  int st = g1_decompress(p, C.raw + (size_t)c * C.raw_stride + 48 * j);
+  if (st == PT_OK && !g1_in_subgroup(p)) st = PT_BAD;
+  if (st == PT_INF) st = PT_BAD;  // KeyValidate rejects the identity
+  uint32_t* q = C.pts + (size_t)t * 24;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { q[k] = p.x.v[k]; q[12 + k] = p.y.v[k]; }
+  C.key_status[t] = (uint8_t)st;
+}
+
+// per committee: sum of all valid keys (for the complement trick) and the invalid-key bitmap
+LCV_FN void item_committee_sum(uint32_t c, const CommitteeDev& C) {
+  g1j acc;
+  jac_set_inf(acc);
+  const uint32_t* pts = C.pts + (size_t)c * 512 * 24;
+  LCV_NOUNROLL for (int w = 0; w < 16; ++w) {
+    uint32_t m = 0;
+    LCV_NOUNROLL for (int b = 0; b < 32; ++b) {
+      const int j = 32 * w + b;
+      if (C.key_status[(size_t)c * 512 + j] != PT_OK) {
+        m |= 1u << b;
+        continue;
+      }
+      g1a p;
+      ld_g1a_tbl(p, pts, j);
+      jac_madd(acc, acc, p);
+    }
+    C.badmask[c * 16 + w] = m;
+  }
+  uint32_t* s = C.sum_all + 36 * c;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { s[k] = acc.x.v[k]; s[12 + k] = acc.y.v[k]; s[24 + k] = acc.z.v[k]; }
+}
+
+}  // namespace lcv

@@ -1,0 +1,119 @@
+"""ctypes binding of the C ABI in include/lcv.h (liblcv.so, HIP/gfx950).
+
+`load()` returns the product library that sits next to this file and raises `LcvUnavailable`
+(loudly) if it is missing or cannot be loaded — there is no CPU fallback anywhere in `lcv`.
+`Lib(path)` binds any library exporting the same ABI; the test suite uses it to drive the
+host-simulation build of the same per-item code (never used by the product path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblcv.so")
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+
+
+class LcvUnavailable(RuntimeError):
+    """liblcv.so (the HIP extension) is missing, unloadable, or no GPU is present."""
+
+
+class LcvError(RuntimeError):
+    pass
+
+
+class HeaderCols(C.Structure):
+    _fields_ = [("beacon", u8p), ("execution", u8p), ("exec_branch", u8p)]
+
+
+class UpdateBatch(C.Structure):
+    _fields_ = [
+        ("attested", HeaderCols),
+        ("finalized", HeaderCols),
+        ("nsc_pool", u8p),
+        ("nsc_index", u32p),
+        ("nsc_branch", u8p),
+        ("finality_branch", u8p),
+        ("sync_bits", u8p),
+        ("sync_signature", u8p),
+        ("signature_slot", u64p),
+        ("n", C.c_uint64),
+        ("npool", C.c_uint64),
+    ]
+
+
+# name -> (restype, argtypes); must match include/lcv.h exactly (tests/test_abi.py checks it)
+SIGNATURES = {
+    "lcv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "lcv_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "lcv_destroy": (None, [C.c_void_p]),
+    "lcv_last_error": (C.c_char_p, [C.c_void_p]),
+    "lcv_set_store": (C.c_int, [C.c_void_p, C.c_uint64, u8p, u8p, u8p]),
+    "lcv_validate_updates": (C.c_int, [C.c_void_p, C.POINTER(UpdateBatch), C.c_uint64, u8p, u8p, u8p]),
+    "lcv_batch_upload": (C.c_int, [C.c_void_p, C.POINTER(UpdateBatch), C.POINTER(C.c_void_p)]),
+    "lcv_batch_free": (None, [C.c_void_p, C.c_void_p]),
+    "lcv_validate_resident": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u8p, u8p, u8p]),
+    "lcv_validate_resident_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u8p, C.c_void_p]),
+    "lcv_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
+    "lcv_stage_name": (C.c_char_p, [C.c_int]),
+    "lcv_fast_aggregate_verify": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, u8p, C.POINTER(C.c_int)]),
+    "lcv_fast_aggregate_verify_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u32p, u8p, u8p, u8p, C.c_uint64, u8p]),
+    "lcv_merkle_branch_batch": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint32, C.c_uint64, u8p, C.c_uint64, u8p]),
+    "lcv_htr_sync_committee_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p]),
+    "lcv_sk_to_pk_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p]),
+    "lcv_sign_batch": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint64, u8p]),
+    "lcv_debug_fp": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint64, u8p, u8p]),
+    "lcv_debug_hash_to_g2": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, u8p]),
+    "lcv_debug_g2_decompress": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, u8p]),
+    "lcv_debug_aggregate": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u32p, u8p, C.c_uint64, u8p, u8p]),
+    "lcv_debug_pairing": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint64, u8p]),
+}
+
+
+def as_u8(buf) -> np.ndarray:
+    a = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8)
+    return a
+
+
+def ptr(a: np.ndarray, ctype=C.c_uint8):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class Lib:
+    def __init__(self, path: str):
+        if not os.path.exists(path):
+            raise LcvUnavailable(f"{path} not found — build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            self.dll = C.CDLL(path)
+        except OSError as e:
+            raise LcvUnavailable(f"cannot load {path}: {e}") from e
+        self.path = path
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(self.dll, name)
+            fn.restype = res
+            fn.argtypes = args
+
+    def __getattr__(self, name):
+        return getattr(self.dll, name)
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> Lib:
+    """The product HIP library (raises LcvUnavailable if absent)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            _lib = Lib(LIB_PATH)
+        return _lib

@@ -1,0 +1,281 @@
+"""`Verifier`: one device context of liblcv.so and numpy-level wrappers around the C ABI."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, fields
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ._native import Lib, LcvError, UpdateBatch, HeaderCols, as_u8, load, ptr
+
+SYNC_COMMITTEE_BYTES = 24624
+EXEC_RECORD_BYTES = 832
+
+
+@dataclass
+class PackedUpdates:
+    """Structure-of-arrays batch of LightClientUpdates (row i = update i); layouts in include/lcv.h."""
+    att_beacon: np.ndarray       # (n, 112) u8
+    att_exec: np.ndarray         # (n, 832) u8
+    att_branch: np.ndarray       # (n, 128) u8
+    fin_beacon: np.ndarray       # (n, 112) u8
+    fin_exec: np.ndarray         # (n, 832) u8
+    fin_branch: np.ndarray       # (n, 128) u8
+    nsc_pool: np.ndarray         # (npool, 24624) u8
+    nsc_index: np.ndarray        # (n,) u32
+    nsc_branch: np.ndarray       # (n, 160) u8
+    finality_branch: np.ndarray  # (n, 192) u8
+    sync_bits: np.ndarray        # (n, 64) u8
+    sync_signature: np.ndarray   # (n, 96) u8
+    signature_slot: np.ndarray   # (n,) u64
+
+    @property
+    def n(self) -> int:
+        return int(self.att_beacon.shape[0])
+
+    def check(self) -> None:
+        n = self.n
+        shapes = dict(att_beacon=112, att_exec=832, att_branch=128, fin_beacon=112, fin_exec=832, fin_branch=128,
+                      nsc_branch=160, finality_branch=192, sync_bits=64, sync_signature=96)
+        for name, w in shapes.items():
+            a = getattr(self, name)
+            if a.dtype != np.uint8 or a.shape != (n, w) or not a.flags.c_contiguous:
+                raise ValueError(f"{name}: need C-contiguous uint8 ({n}, {w}), got {a.dtype} {a.shape}")
+        if self.nsc_pool.dtype != np.uint8 or self.nsc_pool.ndim != 2 or self.nsc_pool.shape[1] != SYNC_COMMITTEE_BYTES:
+            raise ValueError("nsc_pool: need uint8 (npool, 24624)")
+        if self.nsc_index.dtype != np.uint32 or self.nsc_index.shape != (n,):
+            raise ValueError("nsc_index: need uint32 (n,)")
+        if self.signature_slot.dtype != np.uint64 or self.signature_slot.shape != (n,):
+            raise ValueError("signature_slot: need uint64 (n,)")
+        if n and int(self.nsc_index.max()) >= self.nsc_pool.shape[0]:
+            raise ValueError("nsc_index out of range")
+
+    def slice(self, lo: int, hi: int) -> "PackedUpdates":
+        kw = {}
+        for f in fields(self):
+            a = getattr(self, f.name)
+            kw[f.name] = a if f.name == "nsc_pool" else np.ascontiguousarray(a[lo:hi])
+        return PackedUpdates(**kw)
+
+    def to_c(self) -> Tuple[UpdateBatch, list]:
+        self.check()
+        keep = []
+
+        def P(a, t=C.c_uint8):
+            a = np.ascontiguousarray(a)
+            keep.append(a)
+            return ptr(a, t)
+
+        b = UpdateBatch()
+        b.attested = HeaderCols(P(self.att_beacon), P(self.att_exec), P(self.att_branch))
+        b.finalized = HeaderCols(P(self.fin_beacon), P(self.fin_exec), P(self.fin_branch))
+        b.nsc_pool = P(self.nsc_pool)
+        b.nsc_index = P(self.nsc_index, C.c_uint32)
+        b.nsc_branch = P(self.nsc_branch)
+        b.finality_branch = P(self.finality_branch)
+        b.sync_bits = P(self.sync_bits)
+        b.sync_signature = P(self.sync_signature)
+        b.signature_slot = P(self.signature_slot, C.c_uint64)
+        b.n = self.n
+        b.npool = int(self.nsc_pool.shape[0])
+        return b, keep
+
+
+class ResidentBatch:
+    def __init__(self, verifier: "Verifier", handle: C.c_void_p, n: int):
+        self.v = verifier
+        self.handle = handle
+        self.n = n
+
+    def free(self):
+        if self.handle:
+            self.v.lib.lcv_batch_free(self.v.ctx, self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Verifier:
+    """A liblcv context on one device.  `lib` defaults to the product HIP library."""
+
+    def __init__(self, device: int = 0, lib: Optional[Lib] = None):
+        self.lib = lib if lib is not None else load()
+        self.ctx = C.c_void_p()
+        rc = self.lib.lcv_init(device, C.byref(self.ctx))
+        if rc != 0:
+            raise LcvError(f"lcv_init(device={device}) failed with status {rc}")
+        self.device = device
+
+    # ------------------------------------------------------------------ plumbing
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.lcv_last_error(self.ctx)
+            raise LcvError(f"{what}: status {rc}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.lcv_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_timings(self) -> Dict[str, float]:
+        ms = (C.c_float * 16)()
+        n = C.c_int()
+        self._check(self.lib.lcv_last_timings(self.ctx, ms, 16, C.byref(n)), "lcv_last_timings")
+        return {self.lib.lcv_stage_name(i).decode(): float(ms[i]) for i in range(n.value)}
+
+    # ------------------------------------------------------------------ validation
+    def set_store(self, finalized_slot: int, current_sync_committee: bytes, next_sync_committee: bytes) -> np.ndarray:
+        cur = as_u8(bytes(current_sync_committee))
+        nxt = as_u8(bytes(next_sync_committee))
+        if cur.size != SYNC_COMMITTEE_BYTES or nxt.size != SYNC_COMMITTEE_BYTES:
+            raise ValueError("committees must be 24624-byte SSZ SyncCommittee values")
+        ks = np.zeros(1024, np.uint8)
+        self._check(self.lib.lcv_set_store(self.ctx, int(finalized_slot), ptr(cur), ptr(nxt), ptr(ks)), "lcv_set_store")
+        return ks
+
+    def validate(self, batch: PackedUpdates, current_slot: int, genesis_validators_root: bytes):
+        b, keep = batch.to_c()
+        gvr = as_u8(bytes(genesis_validators_root))
+        v = np.zeros(batch.n, np.uint8)
+        r = np.zeros(batch.n, np.uint8)
+        self._check(self.lib.lcv_validate_updates(self.ctx, C.byref(b), int(current_slot), ptr(gvr), ptr(v), ptr(r)),
+                    "lcv_validate_updates")
+        return v.astype(bool), r
+
+    def upload(self, batch: PackedUpdates) -> ResidentBatch:
+        b, keep = batch.to_c()
+        h = C.c_void_p()
+        self._check(self.lib.lcv_batch_upload(self.ctx, C.byref(b), C.byref(h)), "lcv_batch_upload")
+        return ResidentBatch(self, h, batch.n)
+
+    def validate_resident(self, rb: ResidentBatch, current_slot: int, genesis_validators_root: bytes,
+                          verdict: Optional[np.ndarray] = None, reason: Optional[np.ndarray] = None):
+        gvr = as_u8(bytes(genesis_validators_root))
+        v = verdict if verdict is not None else np.zeros(rb.n, np.uint8)
+        r = reason if reason is not None else np.zeros(rb.n, np.uint8)
+        self._check(self.lib.lcv_validate_resident(self.ctx, rb.handle, int(current_slot), ptr(gvr), ptr(v), ptr(r)),
+                    "lcv_validate_resident")
+        return v, r
+
+    def validate_resident_dev(self, rb: ResidentBatch, current_slot: int, genesis_validators_root: bytes,
+                              verdict_dev_ptr: int):
+        gvr = as_u8(bytes(genesis_validators_root))
+        self._check(self.lib.lcv_validate_resident_dev(self.ctx, rb.handle, int(current_slot), ptr(gvr),
+                                                       C.c_void_p(verdict_dev_ptr)), "lcv_validate_resident_dev")
+
+    # ------------------------------------------------------------------ BLS / SSZ primitives
+    def fast_aggregate_verify(self, pubkeys: Sequence[bytes], message: bytes, signature: bytes) -> bool:
+        pks = as_u8(b"".join(bytes(p) for p in pubkeys)) if len(pubkeys) else np.zeros(1, np.uint8)
+        if any(len(bytes(p)) != 48 for p in pubkeys):
+            return False
+        msg, sig = bytes(message), bytes(signature)
+        if len(msg) != 32 or len(sig) != 96:
+            return False
+        res = C.c_int()
+        self._check(self.lib.lcv_fast_aggregate_verify(self.ctx, ptr(pks), len(pubkeys), ptr(as_u8(msg)),
+                                                       ptr(as_u8(sig)), C.byref(res)), "lcv_fast_aggregate_verify")
+        return bool(res.value)
+
+    def fast_aggregate_verify_batch(self, committees: np.ndarray, committee_id: np.ndarray, bits: np.ndarray,
+                                    msgs: np.ndarray, sigs: np.ndarray) -> np.ndarray:
+        committees = np.ascontiguousarray(committees, np.uint8).reshape(-1, 512 * 48)
+        cid = np.ascontiguousarray(committee_id, np.uint32)
+        bits = np.ascontiguousarray(bits, np.uint8).reshape(-1, 64)
+        msgs = np.ascontiguousarray(msgs, np.uint8).reshape(-1, 32)
+        sigs = np.ascontiguousarray(sigs, np.uint8).reshape(-1, 96)
+        n = cid.shape[0]
+        out = np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_fast_aggregate_verify_batch(self.ctx, ptr(committees), committees.shape[0],
+                                                             ptr(cid, C.c_uint32), ptr(bits), ptr(msgs), ptr(sigs), n,
+                                                             ptr(out)), "lcv_fast_aggregate_verify_batch")
+        return out.astype(bool)
+
+    def merkle_branch_batch(self, leaves: np.ndarray, branches: np.ndarray, depth: int, index: int,
+                            roots: np.ndarray) -> np.ndarray:
+        leaves = np.ascontiguousarray(leaves, np.uint8).reshape(-1, 32)
+        n = leaves.shape[0]
+        branches = np.ascontiguousarray(branches, np.uint8).reshape(n, 32 * depth) if depth else np.zeros((n, 0), np.uint8)
+        roots = np.ascontiguousarray(roots, np.uint8).reshape(n, 32)
+        out = np.zeros(n, np.uint8)
+        br = branches if depth else np.zeros(32, np.uint8)
+        self._check(self.lib.lcv_merkle_branch_batch(self.ctx, ptr(leaves), ptr(np.ascontiguousarray(br)), int(depth),
+                                                     int(index), ptr(roots), n, ptr(out)), "lcv_merkle_branch_batch")
+        return out.astype(bool)
+
+    def htr_sync_committee_batch(self, committees: np.ndarray) -> np.ndarray:
+        committees = np.ascontiguousarray(committees, np.uint8).reshape(-1, SYNC_COMMITTEE_BYTES)
+        n = committees.shape[0]
+        out = np.zeros((n, 32), np.uint8)
+        self._check(self.lib.lcv_htr_sync_committee_batch(self.ctx, ptr(committees), n, ptr(out)),
+                    "lcv_htr_sync_committee_batch")
+        return out
+
+    def sk_to_pk_batch(self, sks: np.ndarray) -> np.ndarray:
+        sks = np.ascontiguousarray(sks, np.uint8).reshape(-1, 32)
+        out = np.zeros((sks.shape[0], 48), np.uint8)
+        self._check(self.lib.lcv_sk_to_pk_batch(self.ctx, ptr(sks), sks.shape[0], ptr(out)), "lcv_sk_to_pk_batch")
+        return out
+
+    def sign_batch(self, sks: np.ndarray, msgs: np.ndarray) -> np.ndarray:
+        sks = np.ascontiguousarray(sks, np.uint8).reshape(-1, 32)
+        msgs = np.ascontiguousarray(msgs, np.uint8).reshape(-1, 32)
+        out = np.zeros((sks.shape[0], 96), np.uint8)
+        self._check(self.lib.lcv_sign_batch(self.ctx, ptr(sks), ptr(msgs), sks.shape[0], ptr(out)), "lcv_sign_batch")
+        return out
+
+    # ------------------------------------------------------------------ parity-test entry points
+    def debug_fp(self, a: np.ndarray, b: np.ndarray):
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1, 48)
+        b = np.ascontiguousarray(b, np.uint8).reshape(-1, 48)
+        n = a.shape[0]
+        out = np.zeros((n, 288), np.uint8)
+        ok = np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_debug_fp(self.ctx, ptr(a), ptr(b), n, ptr(out), ptr(ok)), "lcv_debug_fp")
+        return out, ok
+
+    def debug_hash_to_g2(self, msgs: np.ndarray):
+        msgs = np.ascontiguousarray(msgs, np.uint8).reshape(-1, 32)
+        n = msgs.shape[0]
+        out = np.zeros((n, 192), np.uint8)
+        inf = np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_debug_hash_to_g2(self.ctx, ptr(msgs), n, ptr(out), ptr(inf)), "lcv_debug_hash_to_g2")
+        return out, inf
+
+    def debug_g2_decompress(self, sigs: np.ndarray):
+        sigs = np.ascontiguousarray(sigs, np.uint8).reshape(-1, 96)
+        n = sigs.shape[0]
+        out = np.zeros((n, 192), np.uint8)
+        st = np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_debug_g2_decompress(self.ctx, ptr(sigs), n, ptr(out), ptr(st)),
+                    "lcv_debug_g2_decompress")
+        return out, st
+
+    def debug_aggregate(self, committees: np.ndarray, committee_id: np.ndarray, bits: np.ndarray):
+        committees = np.ascontiguousarray(committees, np.uint8).reshape(-1, 512 * 48)
+        cid = np.ascontiguousarray(committee_id, np.uint32)
+        bits = np.ascontiguousarray(bits, np.uint8).reshape(-1, 64)
+        n = cid.shape[0]
+        out = np.zeros((n, 96), np.uint8)
+        st = np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_debug_aggregate(self.ctx, ptr(committees), committees.shape[0], ptr(cid, C.c_uint32),
+                                                 ptr(bits), n, ptr(out), ptr(st)), "lcv_debug_aggregate")
+        return out, st
+
+    def debug_pairing(self, p96: np.ndarray, q192: np.ndarray) -> np.ndarray:
+        p96 = np.ascontiguousarray(p96, np.uint8).reshape(-1, 96)
+        q192 = np.ascontiguousarray(q192, np.uint8).reshape(-1, 192)
+        n = p96.shape[0]
+        out = np.zeros((n, 576), np.uint8)
+        self._check(self.lib.lcv_debug_pairing(self.ctx, ptr(p96), ptr(q192), n, ptr(out)), "lcv_debug_pairing")
+        return out
