@@ -1,6 +1,8 @@
-// lcv_hip.hip — HIP/gfx950 backend of liblcv.so (the product).  One lane per item; every stage of
-// lcv_items.hpp is one kernel launch on the context's stream; HIP events bracket the stages so the
-// per-stage kernel time is reported by lcv_last_timings() (and cross-checked with rocprofv3).
+// lcv_hip.hip — HIP/gfx950 backend of liblcv.so (the product): streams, memory, events and the
+// C ABI (lcv_driver.inc).  One lane per item; every stage of lcv_items.hpp is one kernel launch on
+// the context's stream; HIP events bracket the stages so the per-stage kernel time is reported by
+// lcv_last_timings() (and cross-checked with rocprofv3).  The kernels themselves live in the
+// lcv_k_*.hip units (one heavy stage per unit so they compile in parallel).
 #include <hip/hip_runtime.h>
 
 #include <new>
@@ -38,12 +40,7 @@ static void be_reset_timings(lcv_ctx* ctx);
 static void be_collect_timings(lcv_ctx* ctx);
 
 #include "lcv_driver.inc"
-
-template <class F>
-__global__ __launch_bounds__(64, 1) void k_items(F f, uint32_t n) {
-  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
-  if (i < n) f(i);
-}
+#include "lcv_launch.hpp"
 
 static int hip_fail(lcv_ctx* ctx, hipError_t e, const char* what) {
   return fail(ctx, LCV_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
@@ -113,9 +110,7 @@ static int be_sync(lcv_ctx* ctx) {
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n) {
   if (n == 0) return LCV_OK;
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  const uint32_t blocks = (n + 63u) / 64u;
-  hipLaunchKernelGGL(k_items<F>, dim3(blocks), dim3(64), 0, ctx->be.stream, f, n);
-  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, lcv_hip_launch<F>(f, n, ctx->be.stream));  // defined in the lcv_k_*.hip kernel units
   return LCV_OK;
 }
 

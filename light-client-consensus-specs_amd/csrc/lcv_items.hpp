@@ -72,7 +72,8 @@ struct Work {
   uint32_t* pk;          // [24][cap] aggregate pubkey affine
   uint8_t* agg_status;   // [cap]
   uint32_t* lines;       // [2][68][72][cap]
-  uint32_t* f;           // [144][cap]
+  uint32_t* f;           // [144][cap]   Miller output, then m, then the pairing value
+  uint32_t* fx;          // [2][144][cap] final-exponentiation temporaries
   uint8_t* pair_ok;      // [cap]
   uint8_t* verdict;      // [cap]
   uint8_t* reason;       // [cap]
@@ -347,37 +348,65 @@ LCV_FN void item_miller(uint32_t i, const Work& W) {
   soa_st_fp12(W.f, W.cap, i, f);
 }
 
-// final exponentiation (result e^3, see lcv_pairing.hpp) and the "== 1" test
-LCV_FN void final_exp(fp12& r, const fp12& f) {
-  fp12 m, t0, t1, t2;
-  final_exp_easy(m, f);
-  fp12_exp_xabs(t0, m);
-  fp12_mul(t0, t0, m);
-  fp12_conj(t0, t0);            // A  = m^(x-1)
-  fp12_exp_xabs(t1, t0);
-  fp12_mul(t1, t1, t0);
-  fp12_conj(t1, t1);            // A2 = A^(x-1)
-  fp12_exp_xabs(t0, t1);
-  fp12_conj(t0, t0);
-  fp12_frob1(t1, t1);
-  fp12_mul(t0, t0, t1);         // B  = A2^(x+p)
-  fp12_exp_xabs(t1, t0);
-  fp12_exp_xabs(t1, t1);        // B^(x^2)
-  fp12_frob2(t2, t0);
-  fp12_mul(t1, t1, t2);
-  fp12_conj(t2, t0);
-  fp12_mul(t1, t1, t2);         // C  = B^(x^2 + p^2 - 1)
-  fp12_cyclotomic_sqr(t0, m);
-  fp12_mul(t0, t0, m);
-  fp12_mul(r, t1, t0);          // C * m^3
-}
+// Final exponentiation (result e^3, see lcv_pairing.hpp) and the "== 1" test, as a chain of small
+// kernels with the Fp12 state in HBM between steps (W.f = slot 0, W.fx = slots 1..2): each step is
+// one exponentiation by |x| or a few Fp12 products, which keeps every kernel small enough to
+// compile quickly and gives per-step timings.  Hard part:
+//   A = m^(x-1), A2 = A^(x-1), B = A2^(x+p), C = B^(x^2+p^2-1), result = C * m^3.
+enum { FX_M = 0, FX_T0 = 1, FX_T1 = 2 };  // fp12 slots: W.f (f, then the result), W.fx[0], W.fx[1]
+LCV_FN uint32_t* fx_slot(const Work& W, int k) { return k == 0 ? W.f : W.fx + (size_t)(k - 1) * 144 * W.cap; }
 
-LCV_FN void item_final_exp(uint32_t i, const Work& W) {
-  fp12 f, r;
+// m = f^((p^6 - 1)(p^2 + 1)), in place (slot FX_M = W.f)
+LCV_FN void item_fexp_easy(uint32_t i, const Work& W) {
+  fp12 f, m;
   soa_ld_fp12(f, W.f, W.cap, i);
-  final_exp(r, f);
-  W.pair_ok[i] = fp12_is_one(r) ? 1 : 0;
-  soa_st_fp12(W.f, W.cap, i, r);  // keep the pairing value for the parity tests
+  final_exp_easy(m, f);
+  soa_st_fp12(W.f, W.cap, i, m);
+}
+// dst = src^|x| (cyclotomic)
+LCV_FN void item_fexp_pow(uint32_t i, const Work& W, int src, int dst) {
+  fp12 a, r;
+  soa_ld_fp12(a, fx_slot(W, src), W.cap, i);
+  fp12_exp_xabs(r, a);
+  soa_st_fp12(fx_slot(W, dst), W.cap, i, r);
+}
+// the glue between the exponentiations (op is wave-uniform)
+LCV_FN void item_fexp_glue(uint32_t i, const Work& W, int op) {
+  fp12 a, b;
+  if (op == 1) {  // T0 = conj(T0 * M)                      (A,  from T0 = m^|x|)
+    soa_ld_fp12(a, fx_slot(W, FX_T0), W.cap, i);
+    soa_ld_fp12(b, fx_slot(W, FX_M), W.cap, i);
+    fp12_mul(a, a, b);
+    fp12_conj(a, a);
+    soa_st_fp12(fx_slot(W, FX_T0), W.cap, i, a);
+  } else if (op == 2) {  // T1 = conj(T1 * T0)               (A2, from T1 = A^|x|)
+    soa_ld_fp12(a, fx_slot(W, FX_T1), W.cap, i);
+    soa_ld_fp12(b, fx_slot(W, FX_T0), W.cap, i);
+    fp12_mul(a, a, b);
+    fp12_conj(a, a);
+    soa_st_fp12(fx_slot(W, FX_T1), W.cap, i, a);
+  } else if (op == 3) {  // T0 = conj(T0) * frob1(T1)        (B,  from T0 = A2^|x|, T1 = A2)
+    soa_ld_fp12(a, fx_slot(W, FX_T0), W.cap, i);
+    soa_ld_fp12(b, fx_slot(W, FX_T1), W.cap, i);
+    fp12_conj(a, a);
+    fp12_frob1(b, b);
+    fp12_mul(a, a, b);
+    soa_st_fp12(fx_slot(W, FX_T0), W.cap, i, a);
+  } else {  // op 4: r = T1 * frob2(T0) * conj(T0) * M^3   (T1 = B^(x^2), T0 = B, M = m)
+    fp12 c;
+    soa_ld_fp12(a, fx_slot(W, FX_T1), W.cap, i);
+    soa_ld_fp12(b, fx_slot(W, FX_T0), W.cap, i);
+    fp12_frob2(c, b);
+    fp12_mul(a, a, c);
+    fp12_conj(c, b);
+    fp12_mul(a, a, c);
+    soa_ld_fp12(b, fx_slot(W, FX_M), W.cap, i);
+    fp12_cyclotomic_sqr(c, b);
+    fp12_mul(c, c, b);
+    fp12_mul(a, a, c);
+    W.pair_ok[i] = fp12_is_one(a) ? 1 : 0;
+    soa_st_fp12(W.f, W.cap, i, a);  // keep the pairing value for the parity tests
+  }
 }
 
 LCV_FN void item_verdict(uint32_t i, const Work& W) {

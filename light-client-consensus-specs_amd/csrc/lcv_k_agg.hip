@@ -1,0 +1,8 @@
+// lcv_k_agg.hip — kernel unit: F_agg F_sum (see lcv_launch.hpp).
+#define LCV_KERNEL_UNIT 1
+#define LCV_HD __device__
+#include "lcv_launch.hpp"
+#include "lcv_functors.hpp"
+
+LCV_INSTANTIATE(F_agg)
+LCV_INSTANTIATE(F_sum)

@@ -1,0 +1,7 @@
+// lcv_k_key.hip — kernel unit: F_key (see lcv_launch.hpp).
+#define LCV_KERNEL_UNIT 1
+#define LCV_HD __device__
+#include "lcv_launch.hpp"
+#include "lcv_functors.hpp"
+
+LCV_INSTANTIATE(F_key)

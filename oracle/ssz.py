@@ -15,6 +15,7 @@ can be exec'd against this module (tests/golden/make_golden.py).
 from __future__ import annotations
 
 import hashlib
+import sys
 from typing import Any, Dict, List, Tuple
 
 
@@ -350,7 +351,11 @@ class Container:
             if issubclass(base, Container) and base is not Container:
                 fields = list(base._fields)
         ann = cls.__dict__.get("__annotations__", {})
+        mod = sys.modules.get(cls.__module__)
+        scope = dict(vars(mod)) if mod is not None else {}
         for name, t in ann.items():
+            if isinstance(t, str):  # `from __future__ import annotations` in the defining module
+                t = eval(t, scope)
             fields.append((name, t))
         cls._fields = fields
 
