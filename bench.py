@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: verified LightClientUpdates/sec (512-member committee) on 1..8 MI355X.
+
+One step = `validate_light_client_updates` over this rank's resident batch of synthetic
+mainnet-preset Deneb updates (BASELINE.json configs[1]: 10,000 updates per GPU, full 512/512
+participation, every update carrying next_sync_committee + finality + execution branches), i.e.
+every kernel of the hot path (SSZ/SHA-256, hash_to_G2, signature decode + subgroup check, masked G1
+aggregation, Miller loop, final exponentiation, verdicts).  Inputs are resident in HBM (uploaded
+once, outside the timed region); for N > 1 each step ends with an RCCL all-gather of the per-rank
+verdict bytes (the only collective of the design).  Weak scaling: every rank owns `--n` updates.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n UPDATES_PER_GPU] [--participation full|random]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "light-client-consensus-specs_amd"))
+
+import numpy as np  # noqa: E402
+
+PEAK_INT32_TOPS = 39.3  # 256 CU x 64 lanes x 2.4 GHz; the box-measured mad rate is reported beside it
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sample: int, seed: int = 3):
+    """The CPU oracle (oracle/, a pure-Python restatement of the path) timed on this host, one core,
+    on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import helpers as H
+    from lcv import synth
+    v = H.hostsim_verifier() if os.path.exists(H.HOSTSIM) else None
+    if v is None:
+        return None
+    sb = synth.generate(v, sample, seed=seed)
+    store = H.store_from(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    ups = [H.update_from(sb.updates, i) for i in range(sample)]
+    # warm the per-key KeyValidate cache (a per-store cost, like the device's lcv_set_store)
+    H.O.validate_light_client_update(store, ups[0], sb.current_slot, sb.genesis_validators_root)
+    t0 = time.perf_counter()
+    for u in ups:
+        r = H.O.validate_light_client_update(store, u, sb.current_slot, sb.genesis_validators_root)
+        assert r == 0
+    dt = time.perf_counter() - t0
+    return {"value": round(sample / dt, 3), "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} synthetic Deneb updates (512/512, all branches), oracle/sync_protocol.py "
+                      f"single process; committee KeyValidate cache warmed first"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=10000, help="updates per GPU (configs[1]: 10,000)")
+    ap.add_argument("--participation", default="full", choices=["full", "random"])
+    ap.add_argument("--cpu-sample", type=int, default=12)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from lcv import synth
+    from lcv.device import Verifier
+
+    v = Verifier(local)
+    t0 = time.perf_counter()
+    sb = synth.generate(v, args.n, seed=2 + rank, participation=args.participation)
+    log(f"[rank {rank}] generated {args.n} updates in {time.perf_counter() - t0:.1f}s")
+    v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    rb = v.upload(sb.updates)
+    verdict = np.zeros(args.n, np.uint8)
+    reason = np.zeros(args.n, np.uint8)
+
+    if dist is not None:
+        import torch
+        vdev = torch.zeros(args.n, dtype=torch.uint8, device=f"cuda:{local}")
+        gathered = torch.zeros(world * args.n, dtype=torch.uint8, device=f"cuda:{local}")
+
+    def step():
+        if dist is None:
+            v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
+        else:
+            v.validate_resident_dev(rb, sb.current_slot, sb.genesis_validators_root, vdev.data_ptr())
+            dist.all_gather_into_tensor(gathered, vdev)
+
+    def sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    # correctness of what is timed: every synthetic update is valid
+    if dist is None:
+        v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
+        ok_all = bool((verdict == 1).all())
+    else:
+        step()
+        import torch
+        torch.cuda.synchronize()
+        ok_all = bool((gathered == 1).all().item())
+    stage_ms = {k: 0.0 for k in v.last_timings()}
+
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        for k, ms in v.last_timings().items():
+            stage_ms[k] += ms
+    sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # PCIe-inclusive rate (host batch -> device each time), reported beside `value`, never as it
+    t1 = time.perf_counter()
+    v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    pcie_rate = args.n / (time.perf_counter() - t1)
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    total = world * args.n * args.steps
+    stage_avg = {k: round(ms / args.steps, 3) for k, ms in stage_ms.items()}
+    kernel_ms = sum(stage_avg.values())
+    roof = roofline(stage_avg, args.n)
+    out = {
+        "metric": "verified LightClientUpdates/sec (512-member committee)",
+        "value": round(total / dt, 1),
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (381-bit Montgomery Fp on 12x32-bit limbs; SHA-256 words)",
+        "data": "synthetic (mainnet preset, Deneb, device-signed)",
+        "config": {"workload": f"configs[1]: {args.n} updates/GPU, {args.participation} participation, "
+                               f"next_sync_committee + finality + execution branches",
+                   "updates_per_gpu": args.n, "committee": 512, "parallelism": f"dp{world} (independent updates)"},
+        "all_valid": ok_all,
+        "kernel_ms_per_step": round(kernel_ms, 3),
+        "stage_ms_per_step": stage_avg,
+        "pcie_inclusive_updates_per_s_1gpu": round(pcie_rate, 1),
+        "roofline": roof,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+        except Exception as e:  # reported, never fatal to the GPU measurement
+            out["cpu_baseline"] = {"error": repr(e)}
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def roofline(stage_ms: dict, n: int):
+    """Dominant kernel stage vs the INT32 VALU peak.  Algorithmic work per update per stage comes from
+    profiles/opcounts.json (counted by the host-simulation build of the same kernels, tools/opcount.py):
+    W = 600 N_fpmul + 24 N_fpadd + 2100 N_sha (SURVEY.md §8(d) op model)."""
+    path = os.path.join(ROOT, "profiles", "opcounts.json")
+    if not os.path.exists(path) or not stage_ms:
+        return None
+    counts = json.load(open(path))["per_update"]
+    stage = max(stage_ms, key=lambda k: stage_ms[k])
+    c = counts.get(stage)
+    if c is None or stage_ms[stage] <= 0:
+        return None
+    ops = 600 * c["fp_mul"] + 24 * c["fp_add"] + 2100 * c["sha"]
+    achieved = ops * n / (stage_ms[stage] * 1e-3) / 1e12
+    return {"bound": "valu", "kernel": stage, "achieved": round(achieved, 3), "peak": PEAK_INT32_TOPS,
+            "unit": "T INT32 op/s", "frac": round(achieved / PEAK_INT32_TOPS, 4), "traffic": None,
+            "ops_per_update": ops}
+
+
+if __name__ == "__main__":
+    main()

@@ -8,6 +8,7 @@
 #if defined(LCV_HOSTSIM)
 #define LCV_FN static inline
 #define LCV_NOINLINE static __attribute__((noinline))
+#define LCV_OUTLINE static inline
 #define LCV_CMEM static const
 #define LCV_UNROLL _Pragma("GCC unroll 64")
 #define LCV_NOUNROLL _Pragma("GCC unroll 1")
@@ -16,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #define LCV_FN __device__ __forceinline__
 #define LCV_NOINLINE __device__ __noinline__
+#define LCV_OUTLINE static __device__ __noinline__
 #define LCV_CMEM static __constant__ const
 #define LCV_UNROLL _Pragma("unroll")
 #define LCV_NOUNROLL _Pragma("unroll 1")
@@ -31,6 +33,16 @@
 #else
 #define LCV_FP_CALL 1
 #endif
+#endif
+
+// Op counting (test-only host-simulation build with -DLCV_OPCOUNT): Fp multiplications, Fp
+// additions/subtractions/halvings and SHA-256 compressions, per stage -> the roofline numerator.
+#if defined(LCV_HOSTSIM) && defined(LCV_OPCOUNT)
+#include <atomic>
+namespace lcv { extern std::atomic<unsigned long long> g_ops[3]; }
+#define LCV_COUNT(k) ((void)lcv::g_ops[k].fetch_add(1, std::memory_order_relaxed))
+#else
+#define LCV_COUNT(k) ((void)0)
 #endif
 
 #define LCV_COPY12(dst, src) do { LCV_UNROLL for (int _i = 0; _i < 12; ++_i) (dst)[_i] = (src)[_i]; } while (0)

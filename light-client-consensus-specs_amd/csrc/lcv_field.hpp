@@ -48,6 +48,7 @@ LCV_FN void fp_reduce_once(uint32_t r[12], const uint32_t t[12]) {
 }
 
 LCV_FN void fp_add(fp& r, const fp& a, const fp& b) {
+  LCV_COUNT(1);
   uint32_t s[12];
   uint32_t c = 0;
   LCV_UNROLL for (int j = 0; j < 12; ++j) {
@@ -59,6 +60,7 @@ LCV_FN void fp_add(fp& r, const fp& a, const fp& b) {
 }
 
 LCV_FN void fp_sub(fp& r, const fp& a, const fp& b) {
+  LCV_COUNT(1);
   constexpr uint32_t PL[12] = LCV_P_INIT;
   uint32_t d[12];
   uint32_t br = 0;
@@ -83,6 +85,7 @@ LCV_FN void fp_neg(fp& r, const fp& a) {
   fp_sub(r, z, a);
 }
 LCV_FN void fp_half(fp& r, const fp& a) {
+  LCV_COUNT(1);
   constexpr uint32_t PL[12] = LCV_P_INIT;
   const uint32_t m = 0u - (a.v[0] & 1u);
   uint32_t t[12];
@@ -142,7 +145,10 @@ LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
   LCV_COPY12(r.v, x.v);
 }
 #else
-LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) { fp_mul_impl(r.v, a.v, b.v); }
+LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
+  LCV_COUNT(0);
+  fp_mul_impl(r.v, a.v, b.v);
+}
 #endif
 
 LCV_FN void fp_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }

@@ -3,6 +3,7 @@
 // test suite can check the device arithmetic against the oracle.  The product package `lcv` never
 // loads this library; it exists only for tests/ (see DESIGN.md "Testing without a GPU").
 #define LCV_HOSTSIM 1
+#include <atomic>
 #include <chrono>
 #include <new>
 #include <stdlib.h>
@@ -13,9 +14,15 @@
 
 struct lcv_ctx;
 
+#ifdef LCV_OPCOUNT
+namespace lcv { std::atomic<unsigned long long> g_ops[3]; }
+#endif
+
 struct Backend {
   int open_stage = -1;
   std::chrono::steady_clock::time_point t0;
+  unsigned long long ops0[3] = {0, 0, 0};
+  unsigned long long ops[16][3] = {};
 };
 
 static int be_init(lcv_ctx* ctx, int device);
@@ -58,20 +65,36 @@ template <class F> static int be_launch(lcv_ctx*, const F& f, uint32_t n) {
 static void be_stage_begin(lcv_ctx* ctx, int stage) {
   ctx->be.open_stage = stage;
   ctx->be.t0 = std::chrono::steady_clock::now();
+#ifdef LCV_OPCOUNT
+  for (int k = 0; k < 3; ++k) ctx->be.ops0[k] = lcv::g_ops[k].load();
+#endif
 }
 static void be_stage_end(lcv_ctx* ctx, int stage) {
   if (ctx->be.open_stage != stage) return;
   const auto t1 = std::chrono::steady_clock::now();
   ctx->stage_ms[stage] += std::chrono::duration<float, std::milli>(t1 - ctx->be.t0).count();
+#ifdef LCV_OPCOUNT
+  for (int k = 0; k < 3; ++k) ctx->be.ops[stage][k] += lcv::g_ops[k].load() - ctx->be.ops0[k];
+#endif
   ctx->be.open_stage = -1;
 }
 static void be_reset_timings(lcv_ctx* ctx) {
   for (int s = 0; s < ST_COUNT; ++s) ctx->stage_ms[s] = 0.f;
+  for (int s = 0; s < 16; ++s) for (int k = 0; k < 3; ++k) ctx->be.ops[s][k] = 0;
 }
 static void be_collect_timings(lcv_ctx*) {}
 
 extern "C" int lcv_device_count(int* out) {
   if (!out) return LCV_EINVAL;
   *out = 1;
+  return LCV_OK;
+}
+
+// test/tool-only: per-stage operation counts of the last validate call (needs -DLCV_OPCOUNT):
+// out[3 * s + k], k = 0 Fp multiplications, 1 Fp additions/subtractions/halvings, 2 SHA-256 compressions
+extern "C" int lcv_debug_opcounts(lcv_ctx* ctx, unsigned long long* out, int max_stages) {
+  if (!ctx || !out) return LCV_EINVAL;
+  for (int s = 0; s < max_stages && s < 16; ++s)
+    for (int k = 0; k < 3; ++k) out[3 * s + k] = ctx->be.ops[s][k];
   return LCV_OK;
 }

@@ -16,6 +16,7 @@ struct h256 { uint32_t w[8]; };
 LCV_FN uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
 LCV_FN void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
+  LCV_COUNT(2);
   constexpr uint32_t K[64] = LCV_SHA_K_INIT;
   uint32_t w[16];
   LCV_UNROLL for (int t = 0; t < 16; ++t) w[t] = blk[t];

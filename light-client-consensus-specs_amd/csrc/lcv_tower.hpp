@@ -99,7 +99,7 @@ LCV_FN bool fp12_is_one(const fp12& a) {
 LCV_FN void fp12_conj(fp12& r, const fp12& a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
 
 // Karatsuba over Fp6: 3 Fp6 multiplications (18 Fp2).  r may alias a or b.
-LCV_FN void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
+LCV_FN void fp12_mul_inl(fp12& r, const fp12& a, const fp12& b) {
   fp6 t0, t1, s0, s1;
   fp6_mul(t0, a.c0, b.c0);
   fp6_mul(t1, a.c1, b.c1);
@@ -126,7 +126,7 @@ LCV_FN void fp12_sqr(fp12& r, const fp12& a) {
   fp6_add(r.c1, t, t);
 }
 
-LCV_FN void fp12_inv(fp12& r, const fp12& a) {
+LCV_FN void fp12_inv_inl(fp12& r, const fp12& a) {
   fp6 t0, t1;
   fp6_sqr(t0, a.c0);
   fp6_sqr(t1, a.c1);
@@ -137,6 +137,11 @@ LCV_FN void fp12_inv(fp12& r, const fp12& a) {
   fp6_mul(t1, a.c1, t0);
   fp6_neg(r.c1, t1);
 }
+
+// Out-of-line on the device: a full Fp12 product is ~54 Fp multiplications of straight-line code;
+// one shared copy per kernel keeps the final-exponentiation kernels small (and quick to compile).
+LCV_OUTLINE void fp12_mul(fp12& r, const fp12& a, const fp12& b) { fp12_mul_inl(r, a, b); }
+LCV_OUTLINE void fp12_inv(fp12& r, const fp12& a) { fp12_inv_inl(r, a); }
 
 // Frobenius^k: g_i -> conj^k(g_i) * xi^(i (p^k - 1)/6)
 #define LCV_FROB_APPLY(K, g, i, CONJ)            \

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Count the algorithmic work per verified update, per kernel stage, by running the host-simulation
+build of the SAME per-item kernel code with operation counters (build/liblcv_hostsim_ops.so,
+-DLCV_OPCOUNT): Fp multiplications (incl. squarings), Fp additions/subtractions/halvings and SHA-256
+compressions.  Writes profiles/opcounts.json, the roofline numerator bench.py uses.
+
+    python tools/opcount.py [--n 8] [--participation full|random]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "light-client-consensus-specs_amd")
+sys.path.insert(0, PKG)
+
+from lcv import synth  # noqa: E402
+from lcv._native import Lib  # noqa: E402
+from lcv.device import Verifier  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--participation", default="full")
+    args = ap.parse_args()
+    lib = Lib(os.path.join(PKG, "build", "liblcv_hostsim_ops.so"))
+    lib.dll.lcv_debug_opcounts.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+    v = Verifier(lib=lib)
+    sb = synth.generate(v, args.n, seed=2, participation=args.participation)
+    v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    ok, _ = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    assert ok.all()
+    names = list(v.last_timings().keys())
+    buf = (C.c_ulonglong * (3 * len(names)))()
+    lib.dll.lcv_debug_opcounts(v.ctx, buf, len(names))
+    per = {}
+    for s, name in enumerate(names):
+        fm, fa, sh = buf[3 * s], buf[3 * s + 1], buf[3 * s + 2]
+        if fm or fa or sh:
+            per[name] = {"fp_mul": fm / args.n, "fp_add": fa / args.n, "sha": sh / args.n}
+    tot = {k: sum(d[k] for d in per.values()) for k in ("fp_mul", "fp_add", "sha")}
+    out = {"config": f"{args.n} synthetic Deneb updates, {args.participation} participation, all branches "
+                     f"(nsc pool of 1: HTR(next_sync_committee) amortised over the batch)",
+           "op_model": "INT32 ops = 600*fp_mul + 24*fp_add + 2100*sha (SURVEY.md 8(d))",
+           "per_update": per, "total_per_update": tot,
+           "int32_ops_per_update": 600 * tot["fp_mul"] + 24 * tot["fp_add"] + 2100 * tot["sha"]}
+    path = os.path.join(ROOT, "profiles", "opcounts.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
