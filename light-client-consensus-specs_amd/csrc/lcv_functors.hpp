@@ -6,12 +6,17 @@
 
 using namespace lcv;
 
-struct F_nsc { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_nsc(i, B, C, P, W); } };
+struct F_nsc_team {
+  BatchDev B; CommitteeDev C; Work W;
+  static constexpr uint32_t TEAM = NSC_TEAM, LDS_WORDS = NSC_LDS;
+  LCV_HD uint32_t rounds() const { return NSC_ROUNDS; }
+  LCV_HD void operator()(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds) const { item_nsc_team(j, lane, r, lds, B, C, W); }
+};
 struct F_pre { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_pre(i, B, C, P, W); } };
 struct F_h2c { Work W; LCV_HD void operator()(uint32_t i) const { item_h2c(i, W); } };
 struct F_sig { BatchDev B; Work W; LCV_HD void operator()(uint32_t i) const { item_sig(i, B, W); } };
 struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32_t i) const { item_agg(i, B, C, W); } };
-struct F_lines { Work W; uint32_t n; LCV_HD void operator()(uint32_t t) const { item_lines(t, n, W); } };
+struct F_lines { Work W; uint32_t k; LCV_HD void operator()(uint32_t i) const { item_lines(i, k, W); } };
 struct F_miller { Work W; LCV_HD void operator()(uint32_t i) const { item_miller(i, W); } };
 struct F_fexp_easy { Work W; LCV_HD void operator()(uint32_t i) const { item_fexp_easy(i, W); } };
 struct F_fexp_pow { Work W; int src, dst; LCV_HD void operator()(uint32_t i) const { item_fexp_pow(i, W, src, dst); } };

@@ -35,6 +35,10 @@ static int be_d2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes);
 static int be_memset(lcv_ctx* ctx, void* p, int v, size_t bytes);
 static int be_sync(lcv_ctx* ctx);
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
+template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
+static int be_fork(lcv_ctx*) { return 0; }
+static int be_join(lcv_ctx*) { return 0; }
+static void be_use_stream(lcv_ctx*, int) {}
 static void be_stage_begin(lcv_ctx* ctx, int stage);
 static void be_stage_end(lcv_ctx* ctx, int stage);
 static void be_reset_timings(lcv_ctx* ctx);
@@ -60,6 +64,18 @@ static int be_sync(lcv_ctx*) { return LCV_OK; }
 template <class F> static int be_launch(lcv_ctx*, const F& f, uint32_t n) {
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t i = 0; i < (int64_t)n; ++i) f((uint32_t)i);
+  return LCV_OK;
+}
+// team kernels: the rounds of one item run in order; within a round every lane of the team runs
+// (sequentially here, in lockstep on the device) — programs never read a slot written in the same round
+template <class F> static int be_launch_team(lcv_ctx*, const F& f, uint32_t n) {
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    std::vector<uint32_t> lds(F::LDS_WORDS, 0u);
+    const uint32_t R = f.rounds();
+    for (uint32_t r = 0; r < R; ++r)
+      for (uint32_t lane = 0; lane < F::TEAM; ++lane) f((uint32_t)i, lane, r, lds.data());
+  }
   return LCV_OK;
 }
 static void be_stage_begin(lcv_ctx* ctx, int stage) {

@@ -7,7 +7,7 @@
 // consecutive 32-bit words -> coalesced).
 //
 // Stage map onto the reference's validate_light_client_update (sync-protocol.md:386-465):
-//   item_nsc        hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449)
+//   item_nsc_team   hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449)
 //   item_pre        every non-BLS assert (:392-449) + signing root (:460-463) -> first failing reason
 //   item_h2c        hash_to_G2(signing_root)                   -+
 //   item_sig        signature decode + subgroup check           |  bls.FastAggregateVerify (:464)
@@ -110,20 +110,56 @@ LCV_FN void soa_st_h256(uint32_t* base, size_t cap, size_t i, const h256& a) {
 }
 
 // ============================================================================ SSZ stage
-LCV_FN void item_nsc(uint32_t j, const BatchDev& B, const CommitteeDev& C, const Params& P, const Work& W) {
+// hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449), one team per pool row.
+// Team version (64 lanes per committee): lane l hashes keys 8l..8l+7 into a depth-3 subtree root,
+// then 6 rounds halve the 64 roots (ping-pong LDS buffers), and lane 0 mixes in the aggregate key.
+// The all-zero / equals-store tests are split over the lanes (flags reduced by lane 0).
+enum { NSC_TEAM = 64, NSC_ROUNDS = 8, NSC_LDS = 2 * 64 * 8 + 64 };
+LCV_FN void item_nsc_team(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds, const BatchDev& B,
+                          const CommitteeDev& C, const Work& W) {
   const uint8_t* sc = B.nsc_pool + (size_t)K_SC * j;
-  h256 root;
-  htr_sync_committee(root, sc);
-  soa_st_h256(W.nsc_root, W.pool_cap, j, root);
-  const uint32_t* a = (const uint32_t*)sc;
-  const uint32_t* b = (const uint32_t*)C.next_raw;
-  uint32_t orz = 0, dif = 0;
-  for (int k = 0; k < K_SC / 4; ++k) {
-    const uint32_t x = a[k];
-    orz |= x;
-    dif |= x ^ b[k];
+  uint32_t* buf0 = lds;
+  uint32_t* buf1 = lds + 64 * 8;
+  uint32_t* flags = lds + 2 * 64 * 8;
+  if (r == 0) {
+    h256 n[8];
+    LCV_NOUNROLL for (int k = 0; k < 8; ++k) htr_pubkey(n[k], sc + 48 * (8 * lane + k));
+    hash_pair(n[0], n[0], n[1]);
+    hash_pair(n[2], n[2], n[3]);
+    hash_pair(n[4], n[4], n[5]);
+    hash_pair(n[6], n[6], n[7]);
+    hash_pair(n[0], n[0], n[2]);
+    hash_pair(n[4], n[4], n[6]);
+    hash_pair(n[0], n[0], n[4]);
+    LCV_UNROLL for (int k = 0; k < 8; ++k) buf0[8 * lane + k] = n[0].w[k];
+    const uint32_t* a = (const uint32_t*)sc;
+    const uint32_t* b = (const uint32_t*)C.next_raw;
+    uint32_t orz = 0, dif = 0;
+    for (int k = lane; k < K_SC / 4; k += 64) {
+      const uint32_t x = a[k];
+      orz |= x;
+      dif |= x ^ b[k];
+    }
+    flags[lane] = (orz != 0 ? 1u : 0u) | (dif != 0 ? 2u : 0u);
+  } else if (r < 7) {
+    const uint32_t* src = (r & 1) ? buf0 : buf1;
+    uint32_t* dst = (r & 1) ? buf1 : buf0;
+    if (lane < (64u >> r)) {
+      h256 x, y;
+      LCV_UNROLL for (int k = 0; k < 8; ++k) { x.w[k] = src[16 * lane + k]; y.w[k] = src[16 * lane + 8 + k]; }
+      hash_pair(x, x, y);
+      LCV_UNROLL for (int k = 0; k < 8; ++k) dst[8 * lane + k] = x.w[k];
+    }
+  } else if (lane == 0) {  // r == 7: the 6 halving rounds ended in buf0 (r = 6 writes buf0)
+    h256 root, agg;
+    LCV_UNROLL for (int k = 0; k < 8; ++k) root.w[k] = buf0[k];
+    htr_pubkey(agg, sc + 48 * 512);
+    hash_pair(root, root, agg);
+    soa_st_h256(W.nsc_root, W.pool_cap, j, root);
+    uint32_t f = 0;
+    for (int k = 0; k < 64; ++k) f |= flags[k];
+    W.nsc_flags[j] = (uint8_t)(((f & 1u) ? 0u : 1u) | ((f & 2u) ? 0u : 2u));
   }
-  W.nsc_flags[j] = (uint8_t)((orz == 0 ? 1u : 0u) | (dif == 0 ? 2u : 0u));
 }
 
 LCV_FN uint32_t popcount_bits(const uint8_t* bits) {
@@ -295,9 +331,8 @@ LCV_FN void ld_line(line3& L, const Work& W, uint32_t i, uint32_t k, uint32_t st
   soa_ld_fp2(L.c11, W.lines, W.cap, i, line_slot(k, step, 4) / 2);
 }
 
-// t in [0, 2n): k = t / n selects the G2 point (0: H(m), 1: signature), i = t % n
-LCV_FN void item_lines(uint32_t t, uint32_t n, const Work& W) {
-  const uint32_t k = t / n, i = t % n;
+// k selects the G2 point (0: H(m), 1: signature); one launch per k so the two run on two streams
+LCV_FN void item_lines(uint32_t i, uint32_t k, const Work& W) {
   g2a Q;
   ld_g2a(Q, k == 0 ? W.qh : W.qs, W.cap, i);
   const bool qinf = (k == 0) ? (W.qh_inf[i] != 0) : (W.sig_status[i] != PT_OK);

@@ -1,10 +1,10 @@
-// lcv_k_ssz.hip — kernel unit: F_nsc F_pre F_merkle F_htr_sc F_msg_import F_verdict F_export_g2 F_export_g1 F_export_fp12 F_import_pq (see lcv_launch.hpp).
+// lcv_k_ssz.hip — kernel unit: F_nsc_team F_pre F_merkle F_htr_sc F_msg_import F_verdict F_export_g2 F_export_g1 F_export_fp12 F_import_pq (see lcv_launch.hpp).
 #define LCV_KERNEL_UNIT 1
 #define LCV_HD __device__
 #include "lcv_launch.hpp"
 #include "lcv_functors.hpp"
 
-LCV_INSTANTIATE(F_nsc)
+LCV_INSTANTIATE_TEAM(F_nsc_team)
 LCV_INSTANTIATE(F_pre)
 LCV_INSTANTIATE(F_merkle)
 LCV_INSTANTIATE(F_htr_sc)

@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t s);
+template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s);
 
 #ifdef LCV_KERNEL_UNIT
 template <class F>
@@ -20,5 +21,29 @@ template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t
   hipLaunchKernelGGL(k_items<F>, dim3(blocks), dim3(64), 0, s, f, n);
   return hipGetLastError();
 }
+// Team kernels: F::TEAM lanes cooperate on one item (64 / TEAM items per wave), exchanging values
+// through F::LDS_WORDS words of LDS per item; the item's work is f.rounds() rounds separated by
+// barriers (every lane of a team reads what the previous rounds wrote).
+template <class F>
+__global__ __launch_bounds__(64, 1) void k_team(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
+  __shared__ uint32_t lds[G * F::LDS_WORDS];
+  const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
+  const uint32_t item = blockIdx.x * G + team;
+  const bool active = team < G && item < n;
+  uint32_t* my = lds + (team < G ? team : 0) * F::LDS_WORDS;
+  const uint32_t R = f.rounds();
+  for (uint32_t r = 0; r < R; ++r) {
+    if (active) f(item, lane, r, my);
+    __syncthreads();
+  }
+}
+template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s) {
+  constexpr uint32_t G = 64 / F::TEAM;
+  const uint32_t blocks = (n + G - 1) / G;
+  hipLaunchKernelGGL(k_team<F>, dim3(blocks), dim3(64), 0, s, f, n);
+  return hipGetLastError();
+}
 #define LCV_INSTANTIATE(F) template hipError_t lcv_hip_launch<F>(const F&, uint32_t, hipStream_t);
+#define LCV_INSTANTIATE_TEAM(F) template hipError_t lcv_hip_launch_team<F>(const F&, uint32_t, hipStream_t);
 #endif

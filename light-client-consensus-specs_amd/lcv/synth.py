@@ -191,8 +191,12 @@ def _rand_exec(rng: np.random.Generator, deneb: bool) -> bytes:
 
 
 def _header(rng, slot: int):
-    """Random LightClientHeader at `slot` with a valid execution branch (body root derived)."""
-    deneb = slot // SLOTS_PER_EPOCH >= DENEB_FORK_EPOCH
+    """Random LightClientHeader at `slot` with a valid execution branch (body root derived); before
+    Capella the execution header and branch are empty (as upgraded Altair headers are)."""
+    epoch = slot // SLOTS_PER_EPOCH
+    if epoch < CAPELLA_FORK_EPOCH:
+        return slot, bytes(L.EXEC_BYTES), bytes(128), rng.bytes(32)
+    deneb = epoch >= DENEB_FORK_EPOCH
     ex = _rand_exec(rng, deneb)
     br = [rng.bytes(32) for _ in range(4)]
     body = fold_branch(htr_exec_record(ex, deneb), br, 9)
@@ -201,10 +205,11 @@ def _header(rng, slot: int):
 
 def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERIOD, participation: str = "full",
              kinds: Optional[np.ndarray] = None, with_next: bool = True, with_finality: bool = True,
-             committees=None, gvr: Optional[bytes] = None) -> SyntheticBatch:
+             committees=None, gvr: Optional[bytes] = None, sign_next: bool = False) -> SyntheticBatch:
     """n synthetic updates against one store (finalized at the first slot of `period`, both
     committees known).  participation: "full" (512/512) or "random" (popcount uniform in [342,512]).
-    kinds: optional per-row corruption kinds (see K_*)."""
+    kinds: optional per-row corruption kinds (see K_*).  sign_next: signature slots in the next period,
+    signed by the next committee (sync-protocol.md:452-455 selects it)."""
     rng = np.random.default_rng(seed)
     cur, nxt = committees if committees is not None else (make_committee(verifier, 0), make_committee(verifier, 1))
     gvr = gvr if gvr is not None else sha256(b"lcv-synthetic-genesis-validators-root")
@@ -212,7 +217,8 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
     store_fin = period * SLOTS_PER_PERIOD
     nsc_root = htr_sync_committee(nxt.ssz)
     cur_root = htr_sync_committee(cur.ssz)
-    total_sk = sum(cur.sks) % R_ORDER
+    signer = nxt if sign_next else cur
+    total_sk = sum(signer.sks) % R_ORDER
 
     cols = {k: np.zeros((n, w), np.uint8) for k, w in (("att_beacon", 112), ("att_exec", 832), ("att_branch", 128),
                                                        ("fin_beacon", 112), ("fin_exec", 832), ("fin_branch", 128),
@@ -225,6 +231,8 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
         kind = int(kinds[i])
         att_slot = store_fin + 64 + int(rng.integers(0, SLOTS_PER_PERIOD - 256))
         ss = att_slot + 1 + int(rng.integers(0, 64))
+        if sign_next:
+            ss = store_fin + SLOTS_PER_PERIOD + int(rng.integers(0, 64))
         fin_slot = store_fin + int(rng.integers(0, att_slot - store_fin - 32)) if with_finality else 0
         a_slot, a_ex, a_br, a_body = _header(rng, att_slot)
         # sparse state tree (see module docstring)
@@ -267,7 +275,7 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
         if bits.all():
             sks = total_sk
         else:
-            sks = (total_sk - sum(cur.sks[j] for j in np.flatnonzero(bits == 0))) % R_ORDER
+            sks = (total_sk - sum(signer.sks[j] for j in np.flatnonzero(bits == 0))) % R_ORDER
         m = signing_root(a_beacon, ss, gvr)
         if kind == K_BAD_SIG_MESSAGE:
             m = sha256(b"not-the-signing-root" + m)

@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures (run in the build container only; needs /root/reference).
+
+    python tests/golden/make_golden.py
+
+lc_updates.npz — light-client update cases (packed rows, include/lcv.h layouts) with the reason code
+    of the first failing assert of `validate_light_client_update`.  The expected reason of every case
+    is computed TWICE and must agree:
+      (1) by exec'ing the reference's OWN python blocks from /root/reference/sync-protocol.md
+          (compiled with their markdown line numbers; the failing assert's line is mapped to its
+          index among the function's asserts), over the oracle's restatement of the 36 upstream
+          names (oracle/spec.py: SSZ, compute_*, bls = oracle FastAggregateVerify);
+      (2) by the oracle restatement oracle/sync_protocol.py.
+    Nothing from the reference is stored: only inputs and the expected reason codes.
+bls_vectors.npz — hash_to_G2 outputs, G1/G2 decompression cases (valid, identity, bad flags, x >= p,
+    not on curve, not in the subgroup) and FastAggregateVerify verdicts, all from oracle/bls12_381.py.
+"""
+from __future__ import annotations
+
+import ast
+import json
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import helpers as H  # noqa: E402
+
+from lcv import synth  # noqa: E402
+from oracle import bls12_381 as B  # noqa: E402
+from oracle import spec as S  # noqa: E402
+
+REF = "/root/reference/sync-protocol.md"
+COLS = ("att_beacon", "att_exec", "att_branch", "fin_beacon", "fin_exec", "fin_branch", "nsc_branch",
+        "finality_branch", "sync_bits", "sync_signature")
+
+
+# ----------------------------------------------------------------------------- reference exec
+def load_reference():
+    text = open(REF).read()
+    ns = S.reference_namespace()
+    assert_lines = None
+    for m in re.finditer(r"```python\n(.*?)```", text, re.S):
+        start_line = text[:m.start(1)].count("\n") + 1
+        code = m.group(1)
+        exec(compile("\n" * (start_line - 1) + code, "sync-protocol.md", "exec", dont_inherit=True), ns)
+        if code.startswith("def validate_light_client_update"):
+            tree = ast.parse("\n" * (start_line - 1) + code)
+            assert_lines = [(n.lineno, n.end_lineno) for n in ast.walk(tree) if isinstance(n, ast.Assert)]
+    assert_lines = sorted(assert_lines)
+    assert len(assert_lines) == 14, assert_lines
+    return ns, assert_lines
+
+
+def reference_reason(ns, assert_lines, store, update, current_slot, gvr) -> int:
+    import traceback
+    try:
+        ns["validate_light_client_update"](store, update, current_slot, gvr)
+        return 0
+    except AssertionError:
+        tb = traceback.extract_tb(sys.exc_info()[2])
+        lines = [f.lineno for f in tb if f.filename == "sync-protocol.md"]
+        return next(k for k, (a, b) in enumerate(assert_lines) if a <= lines[-1] <= b) + 1
+
+
+def to_reference_objects(ns, p, i, fin_slot, cur, nxt):
+    """The same bytes as the reference's own container classes (exec'd from the markdown)."""
+    ou = H.update_from(p, i)
+    LCH, LCU = ns["LightClientHeader"], ns["LightClientUpdate"]
+
+    def hdr(h):
+        return LCH(beacon=h.beacon, execution=h.execution, execution_branch=h.execution_branch)
+
+    u = LCU(attested_header=hdr(ou.attested_header), next_sync_committee=ou.next_sync_committee,
+            next_sync_committee_branch=ou.next_sync_committee_branch, finalized_header=hdr(ou.finalized_header),
+            finality_branch=ou.finality_branch, sync_aggregate=ou.sync_aggregate, signature_slot=ou.signature_slot)
+    fin = LCH()
+    fin.beacon.slot = fin_slot
+    store = ns["LightClientStore"](finalized_header=fin, current_sync_committee=H.committee_from(cur),
+                                   next_sync_committee=H.committee_from(nxt), best_valid_update=None,
+                                   optimistic_header=LCH(), previous_max_active_participants=0,
+                                   current_max_active_participants=0)
+    return store, u
+
+
+# ----------------------------------------------------------------------------- cases
+class Cases:
+    def __init__(self):
+        self.rows = {k: [] for k in COLS}
+        self.sig_slot, self.pool_row, self.store_fin, self.next_known, self.current_slot, self.name = [], [], [], [], [], []
+
+    def add(self, p, i, name, store_fin, next_known, current_slot, pool_row, **over):
+        for k in COLS:
+            self.rows[k].append(bytes(over.get(k, p.__dict__[k][i].tobytes())))
+        self.sig_slot.append(int(over.get("signature_slot", p.signature_slot[i])))
+        self.pool_row.append(pool_row)
+        self.store_fin.append(store_fin)
+        self.next_known.append(next_known)
+        self.current_slot.append(current_slot)
+        self.name.append(name)
+
+
+def flip(b: bytes, j: int, mask: int = 1) -> bytes:
+    return b[:j] + bytes([b[j] ^ mask]) + b[j + 1:]
+
+
+def build_cases(v):
+    cur, nxt = synth.make_committee(v, 0), synth.make_committee(v, 1)
+    comms = (cur, nxt)
+    C = Cases()
+    P = synth.DENEB_PERIOD * synth.SLOTS_PER_PERIOD
+    # A: Deneb, next committee known; every corruption kind once (+ 2 valid)
+    kinds = np.array([0, 0, 1, 2, 3, 4, 5, 6, 7])
+    a = synth.generate(v, len(kinds), seed=21, participation="random", kinds=kinds, committees=comms)
+    for i, k in enumerate(kinds):
+        C.add(a.updates, i, f"deneb_kind{k}", P, 1, a.current_slot, 1)
+    pa = a.updates
+    big = P + 4 * synth.SLOTS_PER_PERIOD
+    # mutations of the valid row 0
+    C.add(pa, 0, "slot_order_current", P, 1, int(pa.signature_slot[0]) - 1, 1)
+    C.add(pa, 0, "sig_period_skip", P, 1, big, 1, signature_slot=P + 2 * synth.SLOTS_PER_PERIOD + 5)
+    att_slot = int.from_bytes(pa.att_beacon[0][:8].tobytes(), "little")
+    C.add(pa, 0, "not_relevant", att_slot, 1, a.current_slot, 1)
+    C.add(pa, 0, "finalized_not_empty", P, 1, a.current_slot, 1, finality_branch=bytes(192))
+    fb = bytearray(pa.fin_beacon[0].tobytes())
+    fb[0:8] = bytes(8)
+    C.add(pa, 0, "finalized_genesis_not_empty", P, 1, a.current_slot, 1, fin_beacon=bytes(fb))
+    C.add(pa, 0, "finalized_header_invalid", P, 1, a.current_slot, 1, fin_branch=flip(pa.fin_branch[0].tobytes(), 3))
+    C.add(pa, 0, "nsc_not_empty", P, 1, a.current_slot, 1, nsc_branch=bytes(160))
+    C.add(pa, 0, "nsc_mismatch_store", P, 1, a.current_slot, 0)  # pool row 0 = current committee != store.next
+    C.add(pa, 0, "bad_sig_bitflip", P, 1, a.current_slot, 1, sync_signature=flip(pa.sync_signature[0].tobytes(), 95))
+    sig_inf = bytes([0xC0]) + bytes(95)
+    C.add(pa, 0, "sig_identity", P, 1, a.current_slot, 1, sync_signature=sig_inf)
+    sig_noflag = bytes([pa.sync_signature[0][0] & 0x7F]) + pa.sync_signature[0][1:].tobytes()
+    C.add(pa, 0, "sig_c_flag_clear", P, 1, a.current_slot, 1, sync_signature=sig_noflag)
+    bits_one = bytearray(64)
+    bits_one[0] = 1
+    C.add(pa, 0, "single_participant_wrong_sig", P, 1, a.current_slot, 1, sync_bits=bytes(bits_one))
+    # B: no finality / no next committee (valid), Deneb
+    b1 = synth.generate(v, 1, seed=22, with_finality=False, committees=comms)
+    C.add(b1.updates, 0, "no_finality", P, 1, b1.current_slot, 1)
+    b2 = synth.generate(v, 1, seed=23, with_next=False, committees=comms)
+    C.add(b2.updates, 0, "no_next_committee", P, 1, b2.current_slot, 2)
+    # C: signature by the next committee (signature period = store + 1)
+    c = synth.generate(v, 2, seed=24, sign_next=True, committees=comms)
+    C.add(c.updates, 0, "next_period_signature", P, 1, c.current_slot, 1)
+    C.add(c.updates, 1, "next_period_signature_store_next_unknown", P, 0, c.current_slot, 1)
+    # D: next committee unknown at the store: valid, and relevance via has_next (att slot <= store slot)
+    d = synth.generate(v, 1, seed=25, committees=comms)
+    C.add(d.updates, 0, "store_next_unknown", P, 0, d.current_slot, 1)
+    att_d = int.from_bytes(d.updates.att_beacon[0][:8].tobytes(), "little")
+    C.add(d.updates, 0, "relevant_via_next_committee", att_d, 0, d.current_slot, 1)
+    C.add(d.updates, 0, "not_relevant_next_known", att_d, 1, d.current_slot, 1)
+    # E: Capella update (BASELINE config 1 substitute) and a Capella header carrying blob gas
+    PC = synth.CAPELLA_PERIOD * synth.SLOTS_PER_PERIOD
+    e = synth.generate(v, 1, seed=26, period=synth.CAPELLA_PERIOD, committees=comms)
+    C.add(e.updates, 0, "capella_valid", PC, 1, e.current_slot, 1)
+    ex = bytearray(e.updates.att_exec[0].tobytes())
+    ex[480] = 1
+    C.add(e.updates, 0, "capella_blob_gas", PC, 1, e.current_slot, 1, att_exec=bytes(ex))
+    # F: pre-Capella (Bellatrix) update: empty execution is valid, a non-empty one is not
+    f = synth.generate(v, 1, seed=27, period=600, committees=comms)
+    PB = 600 * synth.SLOTS_PER_PERIOD
+    C.add(f.updates, 0, "bellatrix_valid", PB, 1, f.current_slot, 1)
+    exb = bytearray(832)
+    exb[0] = 7
+    C.add(f.updates, 0, "bellatrix_nonempty_execution", PB, 1, f.current_slot, 1, att_exec=bytes(exb))
+    return C, cur, nxt, a.genesis_validators_root
+
+
+def main():
+    v = H.hostsim_verifier()
+    ns, assert_lines = load_reference()
+    C, cur, nxt, gvr = build_cases(v)
+    n = len(C.name)
+    pool = np.stack([np.frombuffer(x, np.uint8) for x in (cur.ssz, nxt.ssz, bytes(24624))])
+    arrays = {k: np.stack([np.frombuffer(r, np.uint8) for r in C.rows[k]]) for k in COLS}
+    from lcv.device import PackedUpdates
+    p = PackedUpdates(nsc_pool=pool, nsc_index=np.array(C.pool_row, np.uint32),
+                      signature_slot=np.array(C.sig_slot, np.uint64), **arrays)
+    reasons = []
+    for i in range(n):
+        nk = C.next_known[i]
+        nxt_bytes = nxt.ssz if nk else bytes(24624)
+        store_o = H.store_from(C.store_fin[i], cur.ssz, nxt_bytes)
+        r_oracle = H.O.validate_light_client_update(store_o, H.update_from(p, i), C.current_slot[i], gvr)
+        store_r, u_r = to_reference_objects(ns, p, i, C.store_fin[i], cur.ssz, nxt_bytes)
+        r_ref = reference_reason(ns, assert_lines, store_r, u_r, C.current_slot[i], gvr)
+        assert r_oracle == r_ref, (C.name[i], r_oracle, r_ref)
+        reasons.append(r_ref)
+        print(f"{i:3d} {C.name[i]:45s} reason {r_ref}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "lc_updates.npz"), **arrays, nsc_pool=pool,
+                        nsc_index=np.array(C.pool_row, np.uint32), signature_slot=np.array(C.sig_slot, np.uint64),
+                        store_finalized_slot=np.array(C.store_fin, np.uint64),
+                        store_next_known=np.array(C.next_known, np.uint8),
+                        current_slot=np.array(C.current_slot, np.uint64), expected_reason=np.array(reasons, np.uint8),
+                        genesis_validators_root=np.frombuffer(gvr, np.uint8))
+    json.dump({"cases": C.name, "expected_reason": reasons, "reference_assert_lines": assert_lines},
+              open(os.path.join(HERE, "lc_updates.json"), "w"), indent=1)
+    make_bls_vectors()
+
+
+def make_bls_vectors():
+    rng = np.random.default_rng(99)
+    msgs = [bytes(32), b"\xff" * 32] + [rng.bytes(32) for _ in range(6)]
+    h2c = [b"".join(c.to_bytes(48, "big") for c in (q[0][0], q[0][1], q[1][0], q[1][1]))
+           for q in (B.hash_to_g2(m) for m in msgs)]
+    # G2 signature decoding cases: status 0 ok, 1 identity, 2 invalid (py_ecc rules + subgroup)
+    sigs, st = [], []
+    good = B.sign(12345, msgs[2])
+    sigs += [good]; st += [0]
+    sigs += [bytes([0xC0]) + bytes(95)]; st += [1]
+    sigs += [bytes([0xE0]) + bytes(95)]; st += [2]                       # identity with a_flag
+    sigs += [bytes([good[0] & 0x7F]) + good[1:]]; st += [2]              # c_flag clear
+    sigs += [bytes([good[0] | 0x40]) + good[1:]]; st += [2]              # b_flag on a non-identity
+    sigs += [bytes([0x9A]) + b"\xff" * 47 + bytes(48)]; st += [2]        # x1 >= p
+    xp = (B.P + 5).to_bytes(48, "big")
+    sigs += [bytes([0x80]) + bytes(47) + xp]; st += [2]                  # x0 >= p
+    # on the twist curve but outside G2, and not on the curve at all
+    x = 1
+    while True:
+        x += 1
+        X = (x, 1)
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(X), X), B.B2))
+        if y is not None and not B.g2_in_subgroup((X, y)):
+            sigs += [B.g2_compress((X, y))]; st += [2]
+            break
+    x = 1
+    while True:
+        x += 1
+        X = (x, 3)
+        if B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(X), X), B.B2)) is None:
+            enc = bytearray((3).to_bytes(48, "big") + x.to_bytes(48, "big"))
+            enc[0] |= 0x80
+            sigs += [bytes(enc)]
+            st += [2]
+            break
+    # FastAggregateVerify: (pubkeys, msg, sig) -> verdict
+    sks = [7, 11, 13]
+    pks = [B.sk_to_pk(k) for k in sks]
+    m = msgs[3]
+    agg = B.aggregate_signatures([B.sign(k, m) for k in sks])
+    fav = [(pks, m, agg), (pks[:2], m, agg), (pks, msgs[4], agg), ([], m, agg),
+           (pks + [bytes([0xC0]) + bytes(47)], m, agg)]
+    fav_expect = [B.fast_aggregate_verify(a, b_, c) for a, b_, c in fav]
+    assert fav_expect == [True, False, False, False, False]
+    np.savez_compressed(os.path.join(HERE, "bls_vectors.npz"),
+                        h2c_msg=np.frombuffer(b"".join(msgs), np.uint8).reshape(-1, 32),
+                        h2c_out=np.frombuffer(b"".join(h2c), np.uint8).reshape(-1, 192),
+                        sig=np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 96), sig_status=np.array(st, np.uint8),
+                        fav_pks=np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 48),
+                        fav_msg=np.frombuffer(m, np.uint8), fav_sig=np.frombuffer(agg, np.uint8))
+    print("bls vectors:", len(msgs), "h2c,", len(sigs), "signature decodings")
+
+
+if __name__ == "__main__":
+    main()

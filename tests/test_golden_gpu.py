@@ -1,0 +1,25 @@
+"""GPU: liblcv.so on the MI355X against the golden fixtures (reference-exec'd expected reasons)."""
+import numpy as np
+import pytest
+
+import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+
+def test_update_cases_gpu(gpu_verifier):
+    got, exp = G.run_update_cases(gpu_verifier)
+    assert list(got) == list(exp)
+
+
+def test_bls_vectors_gpu(gpu_verifier):
+    b = G.load_bls()
+    out, inf = gpu_verifier.debug_hash_to_g2(b["h2c_msg"])
+    assert np.array_equal(out, b["h2c_out"]) and not inf.any()
+    _, st = gpu_verifier.debug_g2_decompress(b["sig"])
+    assert list(st) == list(b["sig_status"])
+    pks = [b["fav_pks"][k].tobytes() for k in range(3)]
+    m, s = b["fav_msg"].tobytes(), b["fav_sig"].tobytes()
+    assert gpu_verifier.fast_aggregate_verify(pks, m, s)
+    assert not gpu_verifier.fast_aggregate_verify(pks[:2], m, s)
+    assert not gpu_verifier.fast_aggregate_verify(pks + [bytes([0xC0]) + bytes(47)], m, s)
