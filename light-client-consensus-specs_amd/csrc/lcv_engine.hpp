@@ -1,0 +1,225 @@
+// lcv_engine.hpp — team interpreter for the generated pairing programs (tools/gen_programs.py ->
+// lcv_programs.inc): the Miller loop of e(PK, H(m)) * e(-G1, sig) and the final exponentiation,
+// i.e. the pairing check inside bls.FastAggregateVerify (reference call site sync-protocol.md:464).
+//
+// A program is a list of ROUNDS; in round r, lane t of an update's team (TEAM lanes, 64 / TEAM
+// updates per wave) executes one op:  dst <- A * B (MUL), dst <- A^-1 (INV) or dst <- A (LIN), where
+// A and B are signed small-coefficient combinations of Fp values held in the update's LDS slots (or
+// in the constant table).  Every round reads only values written by earlier rounds (the generator's
+// allocator guarantees it), so a barrier between rounds is the only synchronisation.  The Fp
+// arithmetic is the same 12 x 32-bit Montgomery code as everywhere else (lcv_field.hpp).
+//
+// Encoding (uint16): round header [nA, nB, stride, used], then `used` entries of `stride` words:
+//   dst | 0x1000 (MUL) | 0x2000 (INV),  nA terms,  nB terms;   term = slot | coef << 12 (4-bit signed)
+#pragma once
+#include "lcv_items.hpp"
+
+namespace lcv {
+
+enum { ENG_CONST_BASE = 3072, ENG_SLOT_NONE = 0xFFF, ENG_MUL = 0x1000, ENG_INV = 0x2000 };
+
+struct ProgView {
+  const uint16_t* words;
+  const uint32_t* offs;
+  const uint32_t* consts;  // 12 limbs per constant (Montgomery)
+  uint32_t rounds;
+};
+
+LCV_FN void eng_load(fp& v, const uint32_t* lds, const uint32_t* consts, uint32_t slot) {
+  const uint32_t* src = slot >= ENG_CONST_BASE ? consts + 12 * (slot - ENG_CONST_BASE) : lds + 12 * slot;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) v.v[k] = src[k];
+}
+LCV_FN void eng_store(uint32_t* lds, uint32_t slot, const fp& v) {
+  uint32_t* dst = lds + 12 * slot;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) dst[k] = v.v[k];
+}
+
+// acc = sum_k c_k * value(slot_k), |c_k| <= 8 (0 / SLOT_NONE terms are padding)
+LCV_FN void eng_eval(fp& acc, const uint16_t* t, uint32_t n, const uint32_t* lds, const uint32_t* consts) {
+  fp_zero(acc);
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t w = t[k];
+    const uint32_t slot = w & 0xFFFu;
+    int c = (int)(w >> 12);
+    if (slot == ENG_SLOT_NONE || c == 0) continue;
+    if (c >= 8) c -= 16;
+    fp v, m;
+    eng_load(v, lds, consts, slot);
+    const int a = c < 0 ? -c : c;
+    m = v;
+    for (int j = 1; j < a; ++j) fp_add(m, m, v);
+    if (c > 0) fp_add(acc, acc, m);
+    else fp_sub(acc, acc, m);
+  }
+}
+
+// Variable-time binary extended Euclid on canonical values: r = a^-1 mod p (0 -> 0).  Verification
+// handles public data only, so variable time is acceptable; it is ~10x fewer cycles than a^(p-2).
+LCV_FN bool raw_is_one(const fp& a) {
+  uint32_t x = a.v[0] ^ 1u;
+  LCV_UNROLL for (int i = 1; i < 12; ++i) x |= a.v[i];
+  return x == 0;
+}
+LCV_FN void raw_shr1(fp& a) {
+  LCV_UNROLL for (int j = 0; j < 11; ++j) a.v[j] = (a.v[j] >> 1) | (a.v[j + 1] << 31);
+  a.v[11] >>= 1;
+}
+LCV_FN bool raw_sub(fp& r, const fp& a, const fp& b) {  // r = a - b, returns borrow
+  uint32_t br = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    uint64_t s = (uint64_t)a.v[j] - b.v[j] - br;
+    r.v[j] = (uint32_t)s;
+    br = (uint32_t)(s >> 63);
+  }
+  return br != 0;
+}
+LCV_FN void raw_half_mod(fp& x) {  // x / 2 mod p, x < p
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  if (x.v[0] & 1u) {
+    uint32_t c = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) {
+      uint64_t s = (uint64_t)x.v[j] + PL[j] + c;
+      x.v[j] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+  }
+  raw_shr1(x);
+}
+LCV_FN void raw_sub_mod(fp& r, const fp& a, const fp& b) {  // (a - b) mod p, a, b < p
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  if (raw_sub(r, a, b)) {
+    uint32_t c = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) {
+      uint64_t s = (uint64_t)r.v[j] + PL[j] + c;
+      r.v[j] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+  }
+}
+LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
+  fp u, v, x1, x2, t;
+  fp_from_mont(u, a_mont);
+  if (fp_is_zero(u)) {
+    fp_zero(r);
+    return;
+  }
+  LCV_FP_SET(v, LCV_P_INIT);
+  fp_zero(x1);
+  x1.v[0] = 1;
+  fp_zero(x2);
+  while (!raw_is_one(u) && !raw_is_one(v)) {
+    while ((u.v[0] & 1u) == 0) {
+      raw_shr1(u);
+      raw_half_mod(x1);
+    }
+    while ((v.v[0] & 1u) == 0) {
+      raw_shr1(v);
+      raw_half_mod(x2);
+    }
+    if (!raw_sub(t, u, v)) {  // u >= v
+      u = t;
+      raw_sub_mod(x1, x1, x2);
+    } else {
+      raw_sub(v, v, u);
+      raw_sub_mod(x2, x2, x1);
+    }
+  }
+  fp_to_mont(r, raw_is_one(u) ? x1 : x2);
+}
+
+// one round of a program for lane `lane` of the team whose LDS slots start at `lds`
+LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds) {
+  const uint16_t* rp = P.words + P.offs[r];
+  const uint32_t nA = rp[0], nB = rp[1], stride = rp[2], used = rp[3];
+  if (lane >= used) return;
+  const uint16_t* e = rp + 4 + lane * stride;
+  const uint32_t dst = e[0];
+  fp a;
+  eng_eval(a, e + 1, nA, lds, P.consts);
+  if (dst & ENG_MUL) {
+    fp b;
+    eng_eval(b, e + 1 + nA, nB, lds, P.consts);
+    fp_mul(a, a, b);
+  } else if (dst & ENG_INV) {
+    fp_inv_bingcd(a, a);
+  }
+  eng_store(lds, dst & 0xFFFu, a);
+}
+
+}  // namespace lcv
+
+// ============================================================================ pairing stages
+#include "lcv_programs.inc"
+
+namespace lcv {
+
+// fp2 coefficient g_i (of w^i) -> its fp2 slot in the SoA Fp12 layout of soa_st_fp12 (c0.c0, c0.c1,
+// c0.c2, c1.c0, c1.c1, c1.c2 = g0, g2, g4, g1, g3, g5)
+LCV_FN uint32_t fp12_soa_slot(uint32_t g) { return (g & 1u) ? 3u + (g >> 1) : (g >> 1); }
+
+// Miller loop of both pairings.  Prologue (lane k < 12 loads input k): Q1 = H(m), Q2 = signature,
+// P1 = aggregate pubkey, P2 = -G1; an identity Q_k becomes (Q_k = G2 generator, P_k = (0, 0)), whose
+// lines are Fp2 constants killed by the final exponentiation (e(P, O) = 1).  Epilogue: f -> W.f.
+LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+  if (r == 0) {
+    if (lane >= 12) return;
+    const bool q1_id = W.qh_inf[i] != 0, q2_id = W.sig_status[i] != PT_OK;
+    fp v;
+    if (lane < 8) {
+      const bool id = lane < 4 ? q1_id : q2_id;
+      const uint32_t k = lane & 3u;
+      if (id) {
+        fp2 g;
+        if (k < 2) LCV_FP2_SET(g, LCV_G2X);
+        else LCV_FP2_SET(g, LCV_G2Y);
+        v = (k & 1u) ? g.c1 : g.c0;
+      } else {
+        soa_ld_fp(v, lane < 4 ? W.qh : W.qs, W.cap, i, k);
+      }
+    } else if (lane < 10) {  // P1 = (-x, y) of the aggregate pubkey
+      soa_ld_fp(v, W.pk, W.cap, i, lane - 8);
+      if (lane == 8) fp_neg(v, v);
+      if (q1_id) fp_zero(v);
+    } else {                 // P2 = -G1: (-x, y) = (-G1x, -G1y)
+      if (lane == 10) { LCV_FP_SET(v, LCV_G1X_INIT); fp_neg(v, v); }
+      else LCV_FP_SET(v, LCV_G1NEGY_INIT);
+      if (q2_id) fp_zero(v);
+    }
+    eng_store(lds, lane, v);  // input slots 0..11 in the order of LCV_PROG_MILLER_SLOT_*
+  } else if (r <= P.rounds) {
+    eng_round(P, r - 1, lane, lds);
+  } else if (lane < 12) {
+    fp v;
+    eng_load(v, lds, P.consts, LCV_PROG_MILLER_SLOT_F0_0 + lane);
+    soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), v);
+  }
+}
+
+// Final exponentiation; epilogue stores the pairing value (e^3) and the "== 1" verdict.
+LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+  if (r == 0) {
+    if (lane >= 12) return;
+    fp v;
+    soa_ld_fp(v, W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u));
+    eng_store(lds, LCV_PROG_FEXP_SLOT_F0_0 + lane, v);
+  } else if (r <= P.rounds) {
+    eng_round(P, r - 1, lane, lds);
+  } else if (lane < 12) {
+    fp v;
+    eng_load(v, lds, P.consts, LCV_PROG_FEXP_SLOT_R0_0 + lane);
+    soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), v);
+    if (lane == 0) {
+      fp one;
+      fp_one(one);
+      bool ok = fp_eq(v, one);
+      for (uint32_t k = 1; k < 12; ++k) {
+        fp w;
+        eng_load(w, lds, P.consts, LCV_PROG_FEXP_SLOT_R0_0 + k);
+        ok = ok && fp_is_zero(w);
+      }
+      W.pair_ok[i] = ok ? 1 : 0;
+    }
+  }
+}
+
+}  // namespace lcv

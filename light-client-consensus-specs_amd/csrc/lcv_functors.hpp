@@ -2,7 +2,7 @@
 // same code runs as a HIP kernel (one lane per item, lcv_k_*.hip) or as a host loop (hostsim tests).
 // The including file defines LCV_HD (the call-operator qualifier: __device__ or empty).
 #pragma once
-#include "lcv_items.hpp"
+#include "lcv_engine.hpp"
 
 using namespace lcv;
 
@@ -12,15 +12,23 @@ struct F_nsc_team {
   LCV_HD uint32_t rounds() const { return NSC_ROUNDS; }
   LCV_HD void operator()(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds) const { item_nsc_team(j, lane, r, lds, B, C, W); }
 };
+// pairing programs on the team engine (lcv_engine.hpp); one team of TEAM lanes per update
+struct F_eng_miller {
+  Work W; ProgView P;
+  static constexpr uint32_t TEAM = LCV_PROG_MILLER_TEAM, LDS_WORDS = LCV_PROG_MILLER_SLOTS * 12;
+  LCV_HD uint32_t rounds() const { return P.rounds + 2; }
+  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_miller_team(i, lane, r, lds, P, W); }
+};
+struct F_eng_fexp {
+  Work W; ProgView P;
+  static constexpr uint32_t TEAM = LCV_PROG_FEXP_TEAM, LDS_WORDS = LCV_PROG_FEXP_SLOTS * 12;
+  LCV_HD uint32_t rounds() const { return P.rounds + 2; }
+  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_fexp_team(i, lane, r, lds, P, W); }
+};
 struct F_pre { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_pre(i, B, C, P, W); } };
 struct F_h2c { Work W; LCV_HD void operator()(uint32_t i) const { item_h2c(i, W); } };
 struct F_sig { BatchDev B; Work W; LCV_HD void operator()(uint32_t i) const { item_sig(i, B, W); } };
 struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32_t i) const { item_agg(i, B, C, W); } };
-struct F_lines { Work W; uint32_t k; LCV_HD void operator()(uint32_t i) const { item_lines(i, k, W); } };
-struct F_miller { Work W; LCV_HD void operator()(uint32_t i) const { item_miller(i, W); } };
-struct F_fexp_easy { Work W; LCV_HD void operator()(uint32_t i) const { item_fexp_easy(i, W); } };
-struct F_fexp_pow { Work W; int src, dst; LCV_HD void operator()(uint32_t i) const { item_fexp_pow(i, W, src, dst); } };
-struct F_fexp_glue { Work W; int op; LCV_HD void operator()(uint32_t i) const { item_fexp_glue(i, W, op); } };
 struct F_verdict { Work W; LCV_HD void operator()(uint32_t i) const { item_verdict(i, W); } };
 struct F_key { CommitteeDev C; LCV_HD void operator()(uint32_t t) const { item_committee_key(t, C); } };
 struct F_sum { CommitteeDev C; LCV_HD void operator()(uint32_t c) const { item_committee_sum(c, C); } };

@@ -12,7 +12,7 @@
 //   item_h2c        hash_to_G2(signing_root)                   -+
 //   item_sig        signature decode + subgroup check           |  bls.FastAggregateVerify (:464)
 //   item_agg        masked G1 aggregation of participant keys   |
-//   item_lines / item_miller / item_final_exp   pairing check  -+
+//   item_miller_team / item_fexp_team (lcv_engine.hpp)  pairing  -+
 //   item_verdict    conjunction + reason code
 #pragma once
 #include "lcv_h2c.hpp"
@@ -71,9 +71,7 @@ struct Work {
   uint8_t* sig_status;   // [cap]
   uint32_t* pk;          // [24][cap] aggregate pubkey affine
   uint8_t* agg_status;   // [cap]
-  uint32_t* lines;       // [2][68][72][cap]
-  uint32_t* f;           // [144][cap]   Miller output, then m, then the pairing value
-  uint32_t* fx;          // [2][144][cap] final-exponentiation temporaries
+  uint32_t* f;           // [144][cap]   Miller output, then the pairing value
   uint8_t* pair_ok;      // [cap]
   uint8_t* verdict;      // [cap]
   uint8_t* reason;       // [cap]
@@ -316,132 +314,6 @@ LCV_FN void item_agg(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
   soa_st_fp(W.pk, W.cap, i, 0, a.x);
   soa_st_fp(W.pk, W.cap, i, 1, a.y);
   W.agg_status[i] = (uint8_t)(anybad ? PT_BAD : (inf || pc == 0 ? PT_INF : PT_OK));
-}
-
-LCV_FN size_t line_slot(uint32_t k, uint32_t step, uint32_t e) { return ((size_t)k * LCV_MILLER_STEPS + step) * 6 + e; }
-
-LCV_FN void st_line(const Work& W, uint32_t i, uint32_t k, uint32_t step, const line3& L) {
-  soa_st_fp2(W.lines, W.cap, i, line_slot(k, step, 0) / 2, L.c00);
-  soa_st_fp2(W.lines, W.cap, i, line_slot(k, step, 2) / 2, L.c01);
-  soa_st_fp2(W.lines, W.cap, i, line_slot(k, step, 4) / 2, L.c11);
-}
-LCV_FN void ld_line(line3& L, const Work& W, uint32_t i, uint32_t k, uint32_t step) {
-  soa_ld_fp2(L.c00, W.lines, W.cap, i, line_slot(k, step, 0) / 2);
-  soa_ld_fp2(L.c01, W.lines, W.cap, i, line_slot(k, step, 2) / 2);
-  soa_ld_fp2(L.c11, W.lines, W.cap, i, line_slot(k, step, 4) / 2);
-}
-
-// k selects the G2 point (0: H(m), 1: signature); one launch per k so the two run on two streams
-LCV_FN void item_lines(uint32_t i, uint32_t k, const Work& W) {
-  g2a Q;
-  ld_g2a(Q, k == 0 ? W.qh : W.qs, W.cap, i);
-  const bool qinf = (k == 0) ? (W.qh_inf[i] != 0) : (W.sig_status[i] != PT_OK);
-  g2j T;
-  jac_from_aff(T, Q);
-  uint32_t step = 0;
-  LCV_NOUNROLL for (int b = 62; b >= 0; --b) {
-    line3 L;
-    line_dbl(T, L);
-    if (qinf) { fp2_one(L.c00); fp2_zero(L.c01); fp2_zero(L.c11); }
-    st_line(W, i, k, step++, L);
-    if ((LCV_X_ABS >> b) & 1ull) {
-      line_add(T, L, Q);
-      if (qinf) { fp2_one(L.c00); fp2_zero(L.c01); fp2_zero(L.c11); }
-      st_line(W, i, k, step++, L);
-    }
-  }
-}
-
-LCV_FN void item_miller(uint32_t i, const Work& W) {
-  fp nx0, y0, nx1, y1;
-  soa_ld_fp(nx0, W.pk, W.cap, i, 0);
-  fp_neg(nx0, nx0);
-  soa_ld_fp(y0, W.pk, W.cap, i, 1);
-  LCV_FP_SET(nx1, LCV_G1X_INIT);
-  fp_neg(nx1, nx1);
-  LCV_FP_SET(y1, LCV_G1NEGY_INIT);  // P2 = -G1
-  fp12 f;
-  fp12_one(f);
-  uint32_t step = 0;
-  LCV_NOUNROLL for (int b = 62; b >= 0; --b) {
-    line3 L;
-    fp12_sqr(f, f);
-    ld_line(L, W, i, 0, step);
-    fp12_apply_line(f, L, nx0, y0);
-    ld_line(L, W, i, 1, step);
-    fp12_apply_line(f, L, nx1, y1);
-    ++step;
-    if ((LCV_X_ABS >> b) & 1ull) {
-      ld_line(L, W, i, 0, step);
-      fp12_apply_line(f, L, nx0, y0);
-      ld_line(L, W, i, 1, step);
-      fp12_apply_line(f, L, nx1, y1);
-      ++step;
-    }
-  }
-  fp12_conj(f, f);  // x < 0
-  soa_st_fp12(W.f, W.cap, i, f);
-}
-
-// Final exponentiation (result e^3, see lcv_pairing.hpp) and the "== 1" test, as a chain of small
-// kernels with the Fp12 state in HBM between steps (W.f = slot 0, W.fx = slots 1..2): each step is
-// one exponentiation by |x| or a few Fp12 products, which keeps every kernel small enough to
-// compile quickly and gives per-step timings.  Hard part:
-//   A = m^(x-1), A2 = A^(x-1), B = A2^(x+p), C = B^(x^2+p^2-1), result = C * m^3.
-enum { FX_M = 0, FX_T0 = 1, FX_T1 = 2 };  // fp12 slots: W.f (f, then the result), W.fx[0], W.fx[1]
-LCV_FN uint32_t* fx_slot(const Work& W, int k) { return k == 0 ? W.f : W.fx + (size_t)(k - 1) * 144 * W.cap; }
-
-// m = f^((p^6 - 1)(p^2 + 1)), in place (slot FX_M = W.f)
-LCV_FN void item_fexp_easy(uint32_t i, const Work& W) {
-  fp12 f, m;
-  soa_ld_fp12(f, W.f, W.cap, i);
-  final_exp_easy(m, f);
-  soa_st_fp12(W.f, W.cap, i, m);
-}
-// dst = src^|x| (cyclotomic)
-LCV_FN void item_fexp_pow(uint32_t i, const Work& W, int src, int dst) {
-  fp12 a, r;
-  soa_ld_fp12(a, fx_slot(W, src), W.cap, i);
-  fp12_exp_xabs(r, a);
-  soa_st_fp12(fx_slot(W, dst), W.cap, i, r);
-}
-// the glue between the exponentiations (op is wave-uniform)
-LCV_FN void item_fexp_glue(uint32_t i, const Work& W, int op) {
-  fp12 a, b;
-  if (op == 1) {  // T0 = conj(T0 * M)                      (A,  from T0 = m^|x|)
-    soa_ld_fp12(a, fx_slot(W, FX_T0), W.cap, i);
-    soa_ld_fp12(b, fx_slot(W, FX_M), W.cap, i);
-    fp12_mul(a, a, b);
-    fp12_conj(a, a);
-    soa_st_fp12(fx_slot(W, FX_T0), W.cap, i, a);
-  } else if (op == 2) {  // T1 = conj(T1 * T0)               (A2, from T1 = A^|x|)
-    soa_ld_fp12(a, fx_slot(W, FX_T1), W.cap, i);
-    soa_ld_fp12(b, fx_slot(W, FX_T0), W.cap, i);
-    fp12_mul(a, a, b);
-    fp12_conj(a, a);
-    soa_st_fp12(fx_slot(W, FX_T1), W.cap, i, a);
-  } else if (op == 3) {  // T0 = conj(T0) * frob1(T1)        (B,  from T0 = A2^|x|, T1 = A2)
-    soa_ld_fp12(a, fx_slot(W, FX_T0), W.cap, i);
-    soa_ld_fp12(b, fx_slot(W, FX_T1), W.cap, i);
-    fp12_conj(a, a);
-    fp12_frob1(b, b);
-    fp12_mul(a, a, b);
-    soa_st_fp12(fx_slot(W, FX_T0), W.cap, i, a);
-  } else {  // op 4: r = T1 * frob2(T0) * conj(T0) * M^3   (T1 = B^(x^2), T0 = B, M = m)
-    fp12 c;
-    soa_ld_fp12(a, fx_slot(W, FX_T1), W.cap, i);
-    soa_ld_fp12(b, fx_slot(W, FX_T0), W.cap, i);
-    fp12_frob2(c, b);
-    fp12_mul(a, a, c);
-    fp12_conj(c, b);
-    fp12_mul(a, a, c);
-    soa_ld_fp12(b, fx_slot(W, FX_M), W.cap, i);
-    fp12_cyclotomic_sqr(c, b);
-    fp12_mul(c, c, b);
-    fp12_mul(a, a, c);
-    W.pair_ok[i] = fp12_is_one(a) ? 1 : 0;
-    soa_st_fp12(W.f, W.cap, i, a);  // keep the pairing value for the parity tests
-  }
 }
 
 LCV_FN void item_verdict(uint32_t i, const Work& W) {

@@ -1,0 +1,768 @@
+#!/usr/bin/env python3
+"""Generate the team programs of liblcv.so (csrc/lcv_programs.inc): the Miller loop and the final
+exponentiation of the two-pairing check inside FastAggregateVerify (reference call site
+sync-protocol.md:464), compiled into ROUNDS of independent Fp operations for a team of T lanes.
+
+Why: one lane per update leaves a 10^4-update batch with ~160 waves on a 1,024-SIMD chip, so the
+pairing time is the latency of one lane's serial chain of ~17k Fp multiplications.  Here the Fp12 /
+G2 formulas are TRACED symbolically (the same Karatsuba tower as lcv_tower.hpp): every Fp
+multiplication becomes a MUL op whose operands are small linear combinations (+-coefficients) of
+earlier values; additions are folded into those combinations or into LIN ops.  A list scheduler packs
+the ops into rounds of at most T ops (critical path first); values live in per-update LDS slots
+(linear-scan allocation, a slot is reused only in a later round than its last read, so every round
+reads only what previous rounds wrote).  The device kernel (lcv_engine.hpp) is a small interpreter:
+per round, lane t of a team evaluates its two combinations from LDS, multiplies (Montgomery, 12x32
+limbs), stores the result.  Programs are straight-line (|x| is a constant), so they are data.
+
+The generator also EMULATES every program on random inputs with Python integers and checks the
+outputs against independent formulas (oracle/bls12_381.py), so a scheduling or allocation bug fails
+here, not on the GPU.
+
+    python tools/gen_programs.py [--team 32] [--check]
+"""
+from __future__ import annotations
+
+import argparse
+import heapq
+import os
+import random
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+X_ABS = 0xD201000000010000
+RM = 1 << 384
+KOP = 4            # max terms of a MUL operand combination (longer ones are materialised by LIN ops)
+KLIN = 12          # max terms of one LIN op
+COEF_MAX = 7       # term coefficients are signed 4-bit
+SLOT_NONE = 0xFFF
+CONST_BASE = 3072  # slots >= CONST_BASE index the constant table
+
+
+# ============================================================================ symbolic values
+class Val:
+    __slots__ = ("id", "kind", "a", "b", "name", "const", "round", "slot", "last_use", "readers")
+
+    def __init__(self, vid, kind, a=None, b=None, name=None, const=None):
+        self.id, self.kind, self.a, self.b, self.name, self.const = vid, kind, a, b, name, const
+        self.round, self.slot, self.last_use, self.readers = None, None, -1, []
+
+    def __lt__(self, o):
+        return self.id < o.id
+
+    def __repr__(self):
+        return f"V{self.id}:{self.kind}"
+
+
+class Tracer:
+    def __init__(self):
+        self.vals = []
+        self.consts = {}   # value -> Val
+        self.inputs = {}   # name -> Val
+        self.lin_cache = {}
+
+    def _new(self, kind, **kw):
+        v = Val(len(self.vals), kind, **kw)
+        self.vals.append(v)
+        return v
+
+    def input(self, name):
+        v = self._new("in", name=name)
+        self.inputs[name] = v
+        return F(self, {v: 1})
+
+    def const(self, value):
+        value %= P
+        if value == 0:
+            return F(self, {})
+        if value not in self.consts:
+            self.consts[value] = self._new("const", const=value)
+        return F(self, {self.consts[value]: 1})
+
+    def one(self):
+        return self.const(1)
+
+    def _operand(self, f):
+        if len(f.t) > KOP or any(abs(c) > COEF_MAX for c in f.t.values()):
+            return {self.lin(f): 1}
+        return dict(f.t)
+
+    def lin(self, f, name=None):
+        """Materialise a combination (split into chained LIN ops of <= KLIN terms)."""
+        key = tuple(sorted((v.id, c) for v, c in f.t.items()))
+        if name is None and key in self.lin_cache:
+            return self.lin_cache[key]
+        items = list(f.t.items())
+        big = [(v, c) for v, c in items if abs(c) > COEF_MAX]
+        terms = [(v, c) for v, c in items if abs(c) <= COEF_MAX]
+        for v, c in big:  # large coefficients: split c = q*7 + r through doubling chains
+            s = -1 if c < 0 else 1
+            c = abs(c)
+            while c > COEF_MAX:
+                terms.append((v, s * COEF_MAX))
+                c -= COEF_MAX
+            if c:
+                terms.append((v, s * c))
+        while len(terms) > KLIN:
+            head = terms[:KLIN]
+            hv = self._new("lin", a=list(head))
+            terms = [(hv, 1)] + terms[KLIN:]
+        out = self._new("lin", a=list(terms), name=name)
+        if name is None:
+            self.lin_cache[key] = out
+        return out
+
+    def mul(self, x, y):
+        # constant folding: 0, +-small constants, products of constants
+        if not x.t or not y.t:
+            return F(self, {})
+        cx, cy = x.const_value(), y.const_value()
+        if cx is not None and cy is not None:
+            return self.const(cx * cy)
+        for u, w in ((x, y), (y, x)):
+            c = u.const_value()
+            if c is not None:
+                for small in range(-COEF_MAX, COEF_MAX + 1):
+                    if small and c == small % P:
+                        return w * small
+        a, b = self._operand(x), self._operand(y)
+        return F(self, {self._new("mul", a=a, b=b): 1})
+
+    def inv(self, x):
+        return F(self, {self._new("inv", a=self._operand(x)): 1})
+
+
+def _merge(terms):
+    d = defaultdict(int)
+    for v, c in terms:
+        d[v] += c
+    return {v: c for v, c in d.items() if c}
+
+
+class F:
+    """An Fp value as a linear combination of materialised Vals."""
+    __slots__ = ("tr", "t")
+
+    def __init__(self, tr, t):
+        self.tr, self.t = tr, {v: c for v, c in t.items() if c}
+
+    def const_value(self):
+        if all(v.kind == "const" for v in self.t):
+            return sum(v.const * c for v, c in self.t.items()) % P
+        return None
+
+    def __add__(self, o):
+        d = defaultdict(int, self.t)
+        for v, c in o.t.items():
+            d[v] += c
+        return F(self.tr, d)
+
+    def __sub__(self, o):
+        return self + o * -1
+
+    def __neg__(self):
+        return self * -1
+
+    def __mul__(self, o):
+        if isinstance(o, int):
+            return F(self.tr, {v: c * o for v, c in self.t.items()})
+        return self.tr.mul(self, o)
+
+    def dbl(self):
+        return self * 2
+
+    def mat(self):
+        """Force materialisation (a LIN op) — used for values read by many later products."""
+        if len(self.t) == 1 and next(iter(self.t.values())) == 1:
+            return self
+        return F(self.tr, {self.tr.lin(self): 1})
+
+
+# ============================================================================ tower (as lcv_tower.hpp)
+class Fp2:
+    def __init__(self, c0, c1):
+        self.c0, self.c1 = c0, c1
+
+    def __add__(s, o): return Fp2(s.c0 + o.c0, s.c1 + o.c1)
+    def __sub__(s, o): return Fp2(s.c0 - o.c0, s.c1 - o.c1)
+    def __neg__(s): return Fp2(-s.c0, -s.c1)
+    def scale(s, k): return Fp2(s.c0 * k, s.c1 * k)
+    def conj(s): return Fp2(s.c0, -s.c1)
+    def mul_xi(s): return Fp2(s.c0 - s.c1, s.c0 + s.c1)
+    def mul_fp(s, x): return Fp2(s.c0 * x, s.c1 * x)
+    def mat(s): return Fp2(s.c0.mat(), s.c1.mat())
+
+    def __mul__(a, b):
+        t0 = a.c0 * b.c0
+        t1 = a.c1 * b.c1
+        t2 = (a.c0 + a.c1) * (b.c0 + b.c1)
+        return Fp2(t0 - t1, t2 - t0 - t1)
+
+    def sqr(a):
+        return Fp2((a.c0 + a.c1) * (a.c0 - a.c1), (a.c0 * a.c1).dbl())
+
+    def inv(a):
+        t = (a.c0 * a.c0 + a.c1 * a.c1)
+        ti = a.c0.tr.inv(t)
+        return Fp2(a.c0 * ti, -(a.c1 * ti))
+
+
+class Fp6:
+    def __init__(self, c0, c1, c2):
+        self.c0, self.c1, self.c2 = c0, c1, c2
+
+    def __add__(s, o): return Fp6(s.c0 + o.c0, s.c1 + o.c1, s.c2 + o.c2)
+    def __sub__(s, o): return Fp6(s.c0 - o.c0, s.c1 - o.c1, s.c2 - o.c2)
+    def __neg__(s): return Fp6(-s.c0, -s.c1, -s.c2)
+    def mul_v(s): return Fp6(s.c2.mul_xi(), s.c0, s.c1)
+    def mat(s): return Fp6(s.c0.mat(), s.c1.mat(), s.c2.mat())
+
+    def __mul__(a, b):
+        t0, t1, t2 = a.c0 * b.c0, a.c1 * b.c1, a.c2 * b.c2
+        x0 = ((a.c1 + a.c2) * (b.c1 + b.c2) - t1 - t2).mul_xi() + t0
+        x1 = (a.c0 + a.c1) * (b.c0 + b.c1) - t0 - t1 + t2.mul_xi()
+        x2 = (a.c0 + a.c2) * (b.c0 + b.c2) - t0 - t2 + t1
+        return Fp6(x0, x1, x2)
+
+    def sqr(a):  # Chung-Hasan SQR2: 2 mul + 3 sqr in Fp2
+        s0 = a.c0.sqr()
+        ab = a.c0 * a.c1
+        s1 = ab + ab
+        s2 = (a.c0 - a.c1 + a.c2).sqr()
+        bc = a.c1 * a.c2
+        s3 = bc + bc
+        s4 = a.c2.sqr()
+        return Fp6(s3.mul_xi() + s0, s4.mul_xi() + s1, s1 + s2 + s3 - s0 - s4)
+
+    def inv(a):
+        t0 = a.c0.sqr() - (a.c1 * a.c2).mul_xi()
+        t1 = a.c2.sqr().mul_xi() - a.c0 * a.c1
+        t2 = a.c1.sqr() - a.c0 * a.c2
+        t0, t1, t2 = t0.mat(), t1.mat(), t2.mat()
+        d = ((a.c2 * t1 + a.c1 * t2).mul_xi() + a.c0 * t0).inv()
+        d = d.mat()
+        return Fp6(t0 * d, t1 * d, t2 * d)
+
+
+class Fp12:
+    def __init__(self, c0, c1):
+        self.c0, self.c1 = c0, c1
+
+    def conj(s): return Fp12(s.c0, -s.c1)
+    def mat(s): return Fp12(s.c0.mat(), s.c1.mat())
+
+    def __mul__(a, b):
+        t0, t1 = a.c0 * b.c0, a.c1 * b.c1
+        s = (a.c0 + a.c1) * (b.c0 + b.c1)
+        return Fp12(t0 + t1.mul_v(), s - t0 - t1)
+
+    def sqr(a):
+        t = a.c0 * a.c1
+        s = (a.c0 + a.c1) * (a.c0 + a.c1.mul_v())
+        return Fp12(s - t - t.mul_v(), t + t)
+
+    def inv(a):
+        t = (a.c0 * a.c0 - (a.c1 * a.c1).mul_v()).mat().inv()
+        return Fp12(a.c0 * t, -(a.c1 * t))
+
+    def coeffs(s):  # g0..g5 of w^i
+        return [s.c0.c0, s.c1.c0, s.c0.c1, s.c1.c1, s.c0.c2, s.c1.c2]
+
+    @staticmethod
+    def from_coeffs(g):
+        return Fp12(Fp6(g[0], g[2], g[4]), Fp6(g[1], g[3], g[5]))
+
+    def cyclo_sqr(a):
+        g0, g1, g2, g3, g4, g5 = a.coeffs()
+
+        def fp4_sqr(x0, x1):
+            t0, t1 = x0.sqr(), x1.sqr()
+            t2 = (x0 + x1).sqr() - t0 - t1
+            return t0 + t1.mul_xi(), t2
+
+        A0, A1 = fp4_sqr(g0, g3)
+        B0, B1 = fp4_sqr(g1, g4)
+        C0, C1 = fp4_sqr(g2, g5)
+        xc1 = C1.mul_xi()
+        z = [(A0 - g0).scale(2) + A0, (xc1 + g1).scale(2) + xc1, (B0 - g2).scale(2) + B0,
+             (A1 + g3).scale(2) + A1, (C0 - g4).scale(2) + C0, (B1 + g5).scale(2) + B1]
+        return Fp12.from_coeffs(z)
+
+    def frob(a, k, tr):
+        g = a.coeffs()
+        out = []
+        for i in range(6):
+            gi = g[i].conj() if k % 2 else g[i]
+            out.append(gi * const_fp2(tr, FROB[k][i]) if i else gi)
+        return Fp12.from_coeffs(out)
+
+    def mul_line(f, a, b, c):
+        """f * (a + b v + c v w) (sparse line: coefficients of w^0, w^2, w^3)."""
+        F0, F1 = f.c0, f.c1
+        t0, t1 = F0.c0 * a, F0.c1 * b
+        t2 = F0.c2 * b
+        x = Fp6(t0 + t2.mul_xi(), (F0.c0 + F0.c1) * (a + b) - t0 - t1, t1 + F0.c2 * a)
+        y = Fp6((F1.c2 * c).mul_xi(), F1.c0 * c, F1.c1 * c)
+        h = F0 + F1
+        bc = b + c
+        z = Fp6(h.c0 * a + (h.c2 * bc).mul_xi(), h.c0 * bc + h.c1 * a, h.c1 * bc + h.c2 * a)
+        return Fp12(x + y.mul_v(), z - x - y)
+
+
+def fp2_pow(a, e):
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = ((r[0] * a[0] - r[1] * a[1]) % P, (r[0] * a[1] + r[1] * a[0]) % P)
+        a = ((a[0] * a[0] - a[1] * a[1]) % P, (2 * a[0] * a[1]) % P)
+        e >>= 1
+    return r
+
+
+XI = (1, 1)
+FROB = {k: [fp2_pow(XI, i * (P ** k - 1) // 6) for i in range(6)] for k in (1, 2, 3)}
+
+
+def const_fp2(tr, c):
+    return Fp2(tr.const(c[0]), tr.const(c[1]))
+
+
+def in_fp2(tr, name):
+    return Fp2(tr.input(name + "0"), tr.input(name + "1"))
+
+
+def in_fp12(tr, name):
+    return Fp12.from_coeffs([in_fp2(tr, f"{name}{i}_") for i in range(6)])
+
+
+# ============================================================================ G2 lines (as lcv_pairing.hpp)
+B2X3 = (12, 12)  # 3 * 4(1 + u)
+
+
+def line_dbl(T):
+    """Doubling step of lcv_pairing.hpp::line_dbl with the projective representative scaled by 4
+    (no halvings): T and the line change by Fp2 factors only, which the final exponentiation kills."""
+    X, Y, Z = T
+    XY = X * Y
+    B = Y.sqr()
+    C = Z.sqr()
+    E = C * const_fp2(X.c0.tr, B2X3)
+    Fv = E.scale(3)
+    H = (Y + Z).sqr() - B - C
+    J = X.sqr()
+    L = (B - E, J.scale(3), H)
+    nX = (XY * (B - Fv)).scale(2)
+    nY = (B + Fv).sqr() - E.sqr().scale(12)
+    nZ = (B * H).scale(4)
+    return L, (nX, nY, nZ)
+
+
+def line_add(T, Q):
+    X, Y, Z = T
+    qx, qy = Q
+    theta = Y - qy * Z
+    lam = X - qx * Z
+    C = theta.sqr()
+    D = lam.sqr()
+    E = lam * D
+    Fv = Z * C
+    G = X * D
+    H = E + Fv - G - G
+    L = (theta * qx - lam * qy, theta, lam)
+    nX = lam * H
+    nY = theta * (G - H) - Y * E
+    nZ = Z * E
+    return L, (nX, nY, nZ)
+
+
+def miller_program(tr):
+    """Both Miller loops of e(P1, Q1) * e(P2, Q2) with a shared accumulator.  Inputs are affine
+    Q_k and (-x_P, y_P) of P_k; the prologue maps an identity Q_k to (Q_k = G2 generator, P_k = (0, 0)):
+    its lines are then Fp2 constants, killed by the final exponentiation, i.e. e(P_k, O) = 1."""
+    Q = [(in_fp2(tr, "q1x"), in_fp2(tr, "q1y")), (in_fp2(tr, "q2x"), in_fp2(tr, "q2y"))]
+    nxP = [tr.input("p1nx"), tr.input("p2nx")]
+    yP = [tr.input("p1y"), tr.input("p2y")]
+    one = tr.one()
+    T = [(q[0], q[1], Fp2(one, tr.const(0))) for q in Q]
+    f = None
+    for bit in bin(X_ABS)[3:]:
+        for step in ("dbl", "add") if bit == "1" else ("dbl",):
+            lines = []
+            for k in range(2):
+                L, T[k] = line_dbl(T[k]) if step == "dbl" else line_add(T[k], Q[k])
+                T[k] = tuple(t.mat() for t in T[k])
+                c00, c01, c11 = L
+                lines.append((c00.mat(), c01.mul_fp(nxP[k]).mat(), c11.mul_fp(yP[k]).mat()))
+            f = sparse_step(f, lines, square=(step == "dbl" and f is not None))
+    return f.conj()
+
+
+def sparse_step(f, lines, square):
+    (a1, b1, c1), (a2, b2, c2) = lines
+    if f is None:  # f = 1: f * l1 * l2 = l1 * l2 as a dense element
+        tr = a1.c0.tr
+        z = Fp2(tr.const(0), tr.const(0))
+        one12 = Fp12(Fp6(a1, b1, z), Fp6(z, c1, z))
+        return one12.mul_line(a2, b2, c2).mat()
+    if square:
+        f = f.sqr().mat()
+    f = f.mul_line(a1, b1, c1).mat()
+    f = f.mul_line(a2, b2, c2).mat()
+    return f
+
+
+def fexp_program(tr):
+    """Final exponentiation f^((p^12-1)/r) * 3 (hard part (x-1)^2 (x+p)(x^2+p^2-1) + 3), as lcv_items."""
+    f = in_fp12(tr, "f")
+    t0 = f.inv()
+    t1 = f.conj() * t0
+    m = (t1.frob(2, tr) * t1).mat()
+
+    def exp_x(a):  # a^|x| (cyclotomic)
+        acc = a
+        for bit in bin(X_ABS)[3:]:
+            acc = acc.cyclo_sqr().mat()
+            if bit == "1":
+                acc = (acc * a).mat()
+        return acc
+
+    A = (exp_x(m) * m).conj().mat()
+    A2 = (exp_x(A) * A).conj().mat()
+    Bv = (exp_x(A2).conj() * A2.frob(1, tr)).mat()
+    t = exp_x(exp_x(Bv))
+    C = (t * Bv.frob(2, tr) * Bv.conj()).mat()
+    r = C * (m.cyclo_sqr() * m)
+    return r
+
+
+# ============================================================================ scheduling + allocation
+class Program:
+    def __init__(self, name, tr, outputs, team, state_slots, policy="cp", slack=2, cap=96):
+        self.name, self.tr, self.team, self.policy, self.slack, self.cap = name, tr, team, policy, slack, cap
+        self.outputs = outputs            # list of (name, F)
+        self.state_slots = state_slots    # name -> slot for inputs/outputs sharing storage
+        self.build()
+
+    def build(self):
+        tr, T = self.tr, self.team
+        # output ops: one LIN per output (writes its state slot)
+        self.out_ops = []
+        for name, f in self.outputs:
+            self.out_ops.append(tr.lin(f, name="out:" + name))
+        ops = [v for v in tr.vals if v.kind in ("mul", "lin", "inv")]
+        # dependencies
+        deps = {}
+        for v in ops:
+            terms = list(v.a.items()) if isinstance(v.a, dict) else list(v.a)
+            if v.b:
+                terms += list(v.b.items())
+            deps[v] = {u for u, _ in terms if u.kind in ("mul", "lin", "inv")}
+            for u, _ in terms:
+                u.readers.append(v)
+        # WAR: an output written into an input's slot waits for every reader of that input
+        name_to_input = tr.inputs
+        for v in self.out_ops:
+            nm = v.name[4:]
+            if nm in name_to_input:
+                deps[v] |= {r for r in name_to_input[nm].readers if r is not v}
+        # critical-path priority
+        succ = defaultdict(list)
+        for v, ds in deps.items():
+            for u in ds:
+                succ[u].append(v)
+        prio = {}
+        for v in reversed(ops):
+            prio[v] = 1 + max((prio[s] for s in succ[v]), default=0)
+        if self.policy == "fifo":  # trace order: follows the sequential program, keeps few values live
+            prio = {v: -v.id for v in ops}
+        elif self.policy == "mix":  # trace order, but within a window the critical path first
+            prio = {v: -(v.id // 400) * 100000 + prio[v] for v in ops}
+        # ALAP release: an op becomes eligible only `SLACK` levels before the latest level it can run
+        # at without lengthening the critical path, so off-critical work does not run far ahead and
+        # hold LDS slots (the schedule lag is tracked so eligibility keeps pace with the real rounds)
+        cp_len = max(prio.values()) if prio else 0
+        asap = {}
+        for v in ops:
+            asap[v] = 1 + max((asap[u] for u in deps[v]), default=0)
+        operand_vals = {}
+        readers_of = defaultdict(int)
+        for v in ops:
+            terms = list(v.a.items()) if isinstance(v.a, dict) else list(v.a)
+            if v.b:
+                terms += list(v.b.items())
+            operand_vals[v] = {u for u, _ in terms if u.kind in ("mul", "lin", "inv")}
+            for u in operand_vals[v]:
+                readers_of[u] += 1
+        remaining = {}
+        live = [0]
+        indeg = {v: len(deps[v]) for v in ops}
+        waiting = [(cp_len - prio[v], v.id, v) for v in ops if indeg[v] == 0]
+        heapq.heapify(waiting)
+        ready = []
+        rounds = []
+        r = 0
+        lag = 0
+        while ready or waiting:
+            level = r - lag
+            while waiting and waiting[0][0] - self.slack <= level:
+                _, _, v = heapq.heappop(waiting)
+                heapq.heappush(ready, (-prio[v], v.id, v))
+            if not ready:  # nothing eligible: advance the level to the next waiting op
+                lag = r - (waiting[0][0] - self.slack)
+                continue
+            cur, deferred = [], []
+            while ready and len(cur) < T:
+                item = heapq.heappop(ready)
+                v = item[2]
+                ins = {u for u in operand_vals[v] if u in remaining}
+                frees = sum(1 for u in ins if remaining[u] == 1)
+                if cur and live[0] + 1 - frees > self.cap and frees == 0:
+                    deferred.append(item)  # register (LDS slot) pressure: wait for values to die
+                    continue
+                cur.append(v)
+                live[0] += 1 - frees
+                for u in ins:
+                    remaining[u] -= 1
+                    if remaining[u] == 0:
+                        del remaining[u]
+                if readers_of[v]:
+                    remaining[v] = readers_of[v]
+                else:
+                    live[0] -= 1
+            for item in deferred:
+                heapq.heappush(ready, item)
+            for v in cur:
+                v.round = r
+            rounds.append(cur)
+            for v in cur:
+                for s in succ[v]:
+                    indeg[s] -= 1
+                    if indeg[s] == 0:
+                        heapq.heappush(waiting, (cp_len - prio[s], s.id, s))
+            r += 1
+            # critical-path ops still queued: the schedule is behind the ideal levels
+            if ready and min(-p for p, _, _ in ready) >= cp_len - level:
+                lag += 1
+        self.rounds = rounds
+        # last use of every value (round of its last reader)
+        for v in tr.vals:
+            v.last_use = max((u.round for u in v.readers if u.round is not None), default=-1)
+        # slot allocation
+        nxt = 0
+        for name, v in tr.inputs.items():
+            v.slot = self.state_slots[name]
+            nxt = max(nxt, v.slot + 1)
+        for k, (value, v) in enumerate(tr.consts.items()):
+            v.slot = CONST_BASE + k
+        self.consts = [v.const for v in tr.consts.values()]
+        assert len(self.consts) < 4095 - CONST_BASE
+        free = []
+        heapq.heapify(free)
+        nxt = max(nxt, max(self.state_slots.values()) + 1)
+        base_free = nxt
+        release = defaultdict(list)
+        for v in tr.inputs.values():  # inputs whose slots are not reused by outputs may be freed after last use
+            pass
+        peak = nxt
+        for r, cur in enumerate(rounds):
+            for s in release.pop(r, []):
+                heapq.heappush(free, s)
+            for v in cur:
+                if v.name and v.name.startswith("out:"):
+                    v.slot = self.state_slots[v.name[4:]]
+                    continue
+                if free:
+                    v.slot = heapq.heappop(free)
+                else:
+                    v.slot = base_free
+                    base_free += 1
+                    peak = max(peak, base_free)
+                release[max(v.last_use, r) + 1].append(v.slot)
+        self.nslots = peak
+        assert self.nslots < CONST_BASE
+
+    def stats(self):
+        muls = sum(1 for cur in self.rounds for v in cur if v.kind == "mul")
+        lins = sum(1 for cur in self.rounds for v in cur if v.kind == "lin")
+        invs = sum(1 for cur in self.rounds for v in cur if v.kind == "inv")
+        lanes = len(self.rounds) * self.team
+        return (f"{self.name}: team {self.team}, {len(self.rounds)} rounds, {muls} mul, {lins} lin, {invs} inv, "
+                f"lane use {100.0 * (muls + lins + invs) / lanes:.1f}%, {self.nslots} LDS slots "
+                f"({self.nslots * 48} B/item), {len(self.consts)} constants")
+
+    # ---------------------------------------------------------------- encoding
+    def encode(self):
+        """uint16 words.  Round r at offs[r]: [nA, nB, stride, used] then `used` lane entries of
+        `stride` words: dst | flags, nA terms, nB terms.  dst bits 0-11 slot, bit 12 MUL, bit 13 INV.
+        term = slot (bits 0-11) | coef (bits 12-15, two's complement, 0 = no term)."""
+        words, offs = [], []
+        for cur in self.rounds:
+            ents = []
+            for v in cur:
+                a = list(v.a.items()) if isinstance(v.a, dict) else list(v.a)
+                b = list(v.b.items()) if v.b else []
+                ents.append((v, a, b))
+            nA = max(len(a) for _, a, _ in ents)
+            nB = max(len(b) for _, _, b in ents)
+            stride = 1 + nA + nB
+            offs.append(len(words))
+            words += [nA, nB, stride, len(ents)]
+            for v, a, b in ents:
+                flags = (1 << 12) if v.kind == "mul" else (1 << 13) if v.kind == "inv" else 0
+                words.append(v.slot | flags)
+                for terms, n in ((a, nA), (b, nB)):
+                    for u, c in terms:
+                        assert -8 <= c <= 7 and c != 0, c
+                        words.append(u.slot | ((c & 0xF) << 12))
+                    words += [SLOT_NONE] * (n - len(terms))
+        return words, offs
+
+    # ---------------------------------------------------------------- emulation (round semantics)
+    def emulate(self, inputs):
+        mem = {}
+        for name, v in self.tr.inputs.items():
+            mem[v.slot] = inputs[name] % P
+        consts = {CONST_BASE + k: c for k, c in enumerate(self.consts)}
+        words, offs = self.encode()
+        for r, off in enumerate(offs):
+            nA, nB, stride, used = words[off:off + 4]
+            writes = []
+            for lane in range(used):
+                e = words[off + 4 + lane * stride: off + 4 + (lane + 1) * stride]
+                dst = e[0]
+
+                def ev(ts):
+                    acc = 0
+                    for t in ts:
+                        s, c = t & 0xFFF, (t >> 12) & 0xF
+                        if s == SLOT_NONE or c == 0:
+                            continue
+                        c = c - 16 if c >= 8 else c
+                        val = consts[s] if s >= CONST_BASE else mem[s]
+                        acc = (acc + c * val) % P
+                    return acc
+                A = ev(e[1:1 + nA])
+                if dst & (1 << 12):
+                    res = A * ev(e[1 + nA:1 + nA + nB]) % P
+                elif dst & (1 << 13):
+                    res = pow(A, P - 2, P)
+                else:
+                    res = A
+                writes.append((dst & 0xFFF, res))
+            for s, x in writes:
+                mem[s] = x
+        return mem
+
+
+# ============================================================================ checks against the oracle
+def check_miller(prog, team):
+    from oracle import bls12_381 as B
+    rnd = random.Random(7)
+    for trial in range(2):
+        a, b = rnd.randrange(1, 1 << 60), rnd.randrange(1, 1 << 60)
+        Pp = B.g1_mul(B.G1_GEN, a)
+        Q1 = B.g2_mul(B.G2_GEN, b)
+        Q2 = B.g2_mul(B.G2_GEN, b + 7)
+        inp = {"q1x0": Q1[0][0], "q1x1": Q1[0][1], "q1y0": Q1[1][0], "q1y1": Q1[1][1],
+               "q2x0": Q2[0][0], "q2x1": Q2[0][1], "q2y0": Q2[1][0], "q2y1": Q2[1][1],
+               "p1nx": (-Pp[0]) % P, "p1y": Pp[1], "p2nx": (-B.G1_GEN[0]) % P, "p2y": (-B.G1_GEN[1]) % P}
+        mem = prog.emulate(inp)
+        g = [(mem[prog.state_slots[f"f{i}_0"]], mem[prog.state_slots[f"f{i}_1"]]) for i in range(6)]
+        got = B.final_exponentiation(B.f12_from_coeffs(g))
+        e1 = B.pairing(Pp, Q1)
+        e2 = B.pairing(B.g1_neg(B.G1_GEN), Q2)
+        exp = B.f12_mul(e1, e2)
+        assert got == exp, "miller program mismatch"
+    print(f"  miller program checked against oracle pairings ({prog.name})")
+
+
+def check_fexp(prog):
+    from oracle import bls12_381 as B
+    rnd = random.Random(9)
+    f = tuple(tuple((rnd.randrange(P), rnd.randrange(P)) for _ in range(3)) for _ in range(2))
+    g = B.f12_coeffs(f)
+    inp = {}
+    for i in range(6):
+        inp[f"f{i}_0"], inp[f"f{i}_1"] = g[i]
+    mem = prog.emulate(inp)
+    out = [(mem[prog.state_slots[f"r{i}_0"]], mem[prog.state_slots[f"r{i}_1"]]) for i in range(6)]
+    e = B.final_exponentiation(f)
+    assert B.f12_from_coeffs(out) == B.f12_mul(B.f12_mul(e, e), e), "fexp program mismatch"
+    print(f"  fexp program checked against oracle final exponentiation ({prog.name})")
+
+
+# ============================================================================ main
+def make_miller(team, policy="cp"):
+    tr = Tracer()
+    f = miller_program(tr)
+    names = [f"f{i}_{j}" for i in range(6) for j in range(2)]
+    outs = []
+    for i, g in enumerate(f.coeffs()):
+        outs += [(f"f{i}_0", g.c0), (f"f{i}_1", g.c1)]
+    inputs = ["q1x0", "q1x1", "q1y0", "q1y1", "q2x0", "q2x1", "q2y0", "q2y1", "p1nx", "p1y", "p2nx", "p2y"]
+    slots = {n: k for k, n in enumerate(inputs + names)}
+    return Program("miller", tr, outs, team, slots, policy)
+
+
+def make_fexp(team, policy="cp"):
+    tr = Tracer()
+    r = fexp_program(tr)
+    outs = []
+    for i, g in enumerate(r.coeffs()):
+        outs += [(f"r{i}_0", g.c0), (f"r{i}_1", g.c1)]
+    ins = [f"f{i}_{j}" for i in range(6) for j in range(2)]
+    slots = {n: k for k, n in enumerate(ins + [o for o, _ in outs])}
+    return Program("fexp", tr, outs, team, slots, policy)
+
+
+def emit(progs, path):
+    lines = ["// GENERATED by tools/gen_programs.py — do not edit.  Team programs (see lcv_engine.hpp).",
+             "#pragma once", "#include <stdint.h>", ""]
+    for p in progs:
+        words, offs = p.encode()
+        N = p.name.upper()
+        lines.append(f"// {p.stats()}")
+        lines.append(f"#define LCV_PROG_{N}_TEAM {p.team}")
+        lines.append(f"#define LCV_PROG_{N}_ROUNDS {len(offs)}")
+        lines.append(f"#define LCV_PROG_{N}_SLOTS {p.nslots}")
+        lines.append(f"#define LCV_PROG_{N}_NCONST {len(p.consts)}")
+        for nm, s in sorted(p.state_slots.items(), key=lambda kv: kv[1]):
+            lines.append(f"#define LCV_PROG_{N}_SLOT_{nm.upper()} {s}")
+        lines.append(f"static const uint16_t kProg_{p.name}_words[{len(words)}] = {{")
+        for i in range(0, len(words), 24):
+            lines.append("  " + ",".join(str(w) for w in words[i:i + 24]) + ",")
+        lines.append("};")
+        lines.append(f"static const uint32_t kProg_{p.name}_offs[{len(offs)}] = {{")
+        for i in range(0, len(offs), 16):
+            lines.append("  " + ",".join(str(o) for o in offs[i:i + 16]) + ",")
+        lines.append("};")
+        # constants: Montgomery form, 12 little-endian 32-bit limbs each
+        lines.append(f"static const uint32_t kProg_{p.name}_consts[{max(1, len(p.consts)) * 12}] = {{")
+        for c in p.consts or [0]:
+            m = c * RM % P
+            lines.append("  " + ",".join(f"0x{(m >> (32 * k)) & 0xffffffff:08x}u" for k in range(12)) + ",")
+        lines.append("};")
+        lines.append("")
+    open(path, "w").write("\n".join(lines) + "\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--team", type=int, default=32)
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--out", default=os.path.join(ROOT, "light-client-consensus-specs_amd", "csrc", "lcv_programs.inc"))
+    args = ap.parse_args()
+    progs = [make_miller(args.team), make_fexp(args.team)]
+    for p in progs:
+        print(p.stats())
+    if args.check:
+        check_miller(progs[0], args.team)
+        check_fexp(progs[1])
+    emit(progs, args.out)
+
+
+if __name__ == "__main__":
+    main()
