@@ -11,22 +11,29 @@
 //
 // Encoding (uint16): round header [nA, nB, stride, used], then `used` entries of `stride` words:
 //   dst | 0x1000 (MUL) | 0x2000 (INV),  nA terms,  nB terms;   term = slot | coef << 12 (4-bit signed)
+// (header words 0/1 carry the round's max |coef| of A/B in bits 8..15; slots >= nslots are constants)
 #pragma once
 #include "lcv_items.hpp"
 
 namespace lcv {
 
-enum { ENG_CONST_BASE = 3072, ENG_SLOT_NONE = 0xFFF, ENG_MUL = 0x1000, ENG_INV = 0x2000 };
+enum { ENG_SLOT_NONE = 0xFFF, ENG_MUL = 0x1000, ENG_INV = 0x2000 };
 
 struct ProgView {
   const uint16_t* words;
   const uint32_t* offs;
-  const uint32_t* consts;  // 12 limbs per constant (Montgomery)
+  const uint32_t* consts;  // 12 limbs per constant (Montgomery), copied into LDS slots nslots..
   uint32_t rounds;
+  uint32_t nslots, nconst;
 };
 
-LCV_FN void eng_load(fp& v, const uint32_t* lds, const uint32_t* consts, uint32_t slot) {
-  const uint32_t* src = slot >= ENG_CONST_BASE ? consts + 12 * (slot - ENG_CONST_BASE) : lds + 12 * slot;
+// prologue helper: the team copies the program's constants into its LDS slots [nslots, nslots+nconst)
+LCV_FN void eng_load_consts(const ProgView& P, uint32_t lane, uint32_t team, uint32_t* lds) {
+  for (uint32_t k = lane; k < 12 * P.nconst; k += team) lds[12 * P.nslots + k] = P.consts[k];
+}
+
+LCV_FN void eng_load(fp& v, const uint32_t* lds, uint32_t slot) {
+  const uint32_t* src = lds + 12 * slot;
   LCV_UNROLL for (int k = 0; k < 12; ++k) v.v[k] = src[k];
 }
 LCV_FN void eng_store(uint32_t* lds, uint32_t slot, const fp& v) {
@@ -34,23 +41,61 @@ LCV_FN void eng_store(uint32_t* lds, uint32_t slot, const fp& v) {
   LCV_UNROLL for (int k = 0; k < 12; ++k) dst[k] = v.v[k];
 }
 
-// acc = sum_k c_k * value(slot_k), |c_k| <= 8 (0 / SLOT_NONE terms are padding)
-LCV_FN void eng_eval(fp& acc, const uint16_t* t, uint32_t n, const uint32_t* lds, const uint32_t* consts) {
-  fp_zero(acc);
+// out = (sum_k c_k * value(slot_k)) mod p.  Branch-free and uniform across the wave: n (terms) and
+// maxc (largest |c| in the round) come from the round header; padding terms have c = 0.  Each term
+// adds |c| copies of v (c > 0) or of p - v (c < 0) into an UNREDUCED 13-limb accumulator
+// (< MAXSUM * p < 2^387, MAXSUM from the generator), reduced once at the end by conditional
+// subtraction of 32p, 16p, ..., p.
+LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t n, uint32_t maxc, const uint32_t* lds) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint32_t acc[13];
+  LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = 0;
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t w = t[k];
-    const uint32_t slot = w & 0xFFFu;
+    uint32_t slot = w & 0xFFFu;
     int c = (int)(w >> 12);
-    if (slot == ENG_SLOT_NONE || c == 0) continue;
     if (c >= 8) c -= 16;
-    fp v, m;
-    eng_load(v, lds, consts, slot);
-    const int a = c < 0 ? -c : c;
-    m = v;
-    for (int j = 1; j < a; ++j) fp_add(m, m, v);
-    if (c > 0) fp_add(acc, acc, m);
-    else fp_sub(acc, acc, m);
+    if (slot == ENG_SLOT_NONE) { slot = 0; c = 0; }
+    const uint32_t* src = lds + 12 * slot;
+    uint32_t v[12], d[12];
+    LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = src[j];
+    uint32_t br = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) {  // d = p - v  (in [1, p])
+      const uint64_t x = (uint64_t)PL[j] - v[j] - br;
+      d[j] = (uint32_t)x;
+      br = (uint32_t)(x >> 63);
+    }
+    const uint32_t a = (uint32_t)(c < 0 ? -c : c);
+    const uint32_t negm = c < 0 ? 0xFFFFFFFFu : 0u;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = (d[j] & negm) | (v[j] & ~negm);
+    for (uint32_t rep = 0; rep < maxc; ++rep) {
+      const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;
+      uint32_t cy = 0;
+      LCV_UNROLL for (int j = 0; j < 12; ++j) {
+        const uint64_t x = (uint64_t)acc[j] + (v[j] & keep) + cy;
+        acc[j] = (uint32_t)x;
+        cy = (uint32_t)(x >> 32);
+      }
+      acc[12] += cy;
+    }
   }
+  LCV_UNROLL for (int s = 5; s >= 0; --s) {  // acc < 64 p  ->  acc mod p
+    uint32_t sp[13], d[13];
+    uint32_t cy = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) {  // sp = p << s
+      sp[j] = (PL[j] << s) | cy;
+      cy = s ? (PL[j] >> (32 - s)) : 0u;
+    }
+    sp[12] = cy;
+    uint32_t br = 0;
+    LCV_UNROLL for (int j = 0; j < 13; ++j) {
+      const uint64_t x = (uint64_t)acc[j] - sp[j] - br;
+      d[j] = (uint32_t)x;
+      br = (uint32_t)(x >> 63);
+    }
+    LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = br ? acc[j] : d[j];
+  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) out.v[j] = acc[j];
 }
 
 // Variable-time binary extended Euclid on canonical values: r = a^-1 mod p (0 -> 0).  Verification
@@ -130,15 +175,16 @@ LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
 // one round of a program for lane `lane` of the team whose LDS slots start at `lds`
 LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds) {
   const uint16_t* rp = P.words + P.offs[r];
-  const uint32_t nA = rp[0], nB = rp[1], stride = rp[2], used = rp[3];
+  const uint32_t hA = rp[0], hB = rp[1], stride = rp[2], used = rp[3];
+  const uint32_t nA = hA & 0xFFu, nB = hB & 0xFFu;
   if (lane >= used) return;
   const uint16_t* e = rp + 4 + lane * stride;
   const uint32_t dst = e[0];
   fp a;
-  eng_eval(a, e + 1, nA, lds, P.consts);
+  eng_eval(a, e + 1, nA, hA >> 8, lds);
   if (dst & ENG_MUL) {
     fp b;
-    eng_eval(b, e + 1 + nA, nB, lds, P.consts);
+    eng_eval(b, e + 1 + nA, nB, hB >> 8, lds);
     fp_mul(a, a, b);
   } else if (dst & ENG_INV) {
     fp_inv_bingcd(a, a);
@@ -162,6 +208,7 @@ LCV_FN uint32_t fp12_soa_slot(uint32_t g) { return (g & 1u) ? 3u + (g >> 1) : (g
 // lines are Fp2 constants killed by the final exponentiation (e(P, O) = 1).  Epilogue: f -> W.f.
 LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
   if (r == 0) {
+    eng_load_consts(P, lane, LCV_PROG_MILLER_TEAM, lds);
     if (lane >= 12) return;
     const bool q1_id = W.qh_inf[i] != 0, q2_id = W.sig_status[i] != PT_OK;
     fp v;
@@ -190,7 +237,7 @@ LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* ld
     eng_round(P, r - 1, lane, lds);
   } else if (lane < 12) {
     fp v;
-    eng_load(v, lds, P.consts, LCV_PROG_MILLER_SLOT_F0_0 + lane);
+    eng_load(v, lds, LCV_PROG_MILLER_SLOT_F0_0 + lane);
     soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), v);
   }
 }
@@ -198,6 +245,7 @@ LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* ld
 // Final exponentiation; epilogue stores the pairing value (e^3) and the "== 1" verdict.
 LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
   if (r == 0) {
+    eng_load_consts(P, lane, LCV_PROG_FEXP_TEAM, lds);
     if (lane >= 12) return;
     fp v;
     soa_ld_fp(v, W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u));
@@ -206,7 +254,7 @@ LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds,
     eng_round(P, r - 1, lane, lds);
   } else if (lane < 12) {
     fp v;
-    eng_load(v, lds, P.consts, LCV_PROG_FEXP_SLOT_R0_0 + lane);
+    eng_load(v, lds, LCV_PROG_FEXP_SLOT_R0_0 + lane);
     soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), v);
     if (lane == 0) {
       fp one;
@@ -214,7 +262,7 @@ LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds,
       bool ok = fp_eq(v, one);
       for (uint32_t k = 1; k < 12; ++k) {
         fp w;
-        eng_load(w, lds, P.consts, LCV_PROG_FEXP_SLOT_R0_0 + k);
+        eng_load(w, lds, LCV_PROG_FEXP_SLOT_R0_0 + k);
         ok = ok && fp_is_zero(w);
       }
       W.pair_ok[i] = ok ? 1 : 0;

@@ -2,7 +2,7 @@
 // same code runs as a HIP kernel (one lane per item, lcv_k_*.hip) or as a host loop (hostsim tests).
 // The including file defines LCV_HD (the call-operator qualifier: __device__ or empty).
 #pragma once
-#include "lcv_engine.hpp"
+#include "lcv_items.hpp"
 
 using namespace lcv;
 
@@ -11,19 +11,6 @@ struct F_nsc_team {
   static constexpr uint32_t TEAM = NSC_TEAM, LDS_WORDS = NSC_LDS;
   LCV_HD uint32_t rounds() const { return NSC_ROUNDS; }
   LCV_HD void operator()(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds) const { item_nsc_team(j, lane, r, lds, B, C, W); }
-};
-// pairing programs on the team engine (lcv_engine.hpp); one team of TEAM lanes per update
-struct F_eng_miller {
-  Work W; ProgView P;
-  static constexpr uint32_t TEAM = LCV_PROG_MILLER_TEAM, LDS_WORDS = LCV_PROG_MILLER_SLOTS * 12;
-  LCV_HD uint32_t rounds() const { return P.rounds + 2; }
-  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_miller_team(i, lane, r, lds, P, W); }
-};
-struct F_eng_fexp {
-  Work W; ProgView P;
-  static constexpr uint32_t TEAM = LCV_PROG_FEXP_TEAM, LDS_WORDS = LCV_PROG_FEXP_SLOTS * 12;
-  LCV_HD uint32_t rounds() const { return P.rounds + 2; }
-  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_fexp_team(i, lane, r, lds, P, W); }
 };
 struct F_pre { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_pre(i, B, C, P, W); } };
 struct F_h2c { Work W; LCV_HD void operator()(uint32_t i) const { item_h2c(i, W); } };

@@ -4,7 +4,7 @@
 #define LCV_KERNEL_UNIT 1
 #define LCV_HD __device__
 #include "lcv_launch.hpp"
-#include "lcv_functors.hpp"
+#include "lcv_functors_eng.hpp"
 
 LCV_INSTANTIATE_TEAM(F_eng_miller)
 LCV_INSTANTIATE_TEAM(F_eng_fexp)

@@ -555,10 +555,7 @@ class Program:
         for name, v in tr.inputs.items():
             v.slot = self.state_slots[name]
             nxt = max(nxt, v.slot + 1)
-        for k, (value, v) in enumerate(tr.consts.items()):
-            v.slot = CONST_BASE + k
         self.consts = [v.const for v in tr.consts.values()]
-        assert len(self.consts) < 4095 - CONST_BASE
         free = []
         heapq.heapify(free)
         nxt = max(nxt, max(self.state_slots.values()) + 1)
@@ -582,7 +579,20 @@ class Program:
                     peak = max(peak, base_free)
                 release[max(v.last_use, r) + 1].append(v.slot)
         self.nslots = peak
-        assert self.nslots < CONST_BASE
+        for k, v in enumerate(tr.consts.values()):  # constants are copied into LDS after the slots
+            v.slot = self.nslots + k
+        assert self.nslots + len(self.consts) < SLOT_NONE
+
+    def max_abs_sum(self):
+        """max over all combinations of sum |coef| (bounds the unreduced accumulator: < sum * p)"""
+        m = 1
+        for cur in self.rounds:
+            for v in cur:
+                for terms in (v.a, v.b):
+                    if terms:
+                        items = terms.items() if isinstance(terms, dict) else terms
+                        m = max(m, sum(abs(c) for _, c in items))
+        return m
 
     def stats(self):
         muls = sum(1 for cur in self.rounds for v in cur if v.kind == "mul")
@@ -595,9 +605,10 @@ class Program:
 
     # ---------------------------------------------------------------- encoding
     def encode(self):
-        """uint16 words.  Round r at offs[r]: [nA, nB, stride, used] then `used` lane entries of
-        `stride` words: dst | flags, nA terms, nB terms.  dst bits 0-11 slot, bit 12 MUL, bit 13 INV.
-        term = slot (bits 0-11) | coef (bits 12-15, two's complement, 0 = no term)."""
+        """uint16 words.  Round r at offs[r]: [nA | maxcA << 8, nB | maxcB << 8, stride, used] then `used`
+        lane entries of `stride` words: dst | flags, nA terms, nB terms.  dst bits 0-11 slot, bit 12
+        MUL, bit 13 INV.  term = slot (bits 0-11) | coef (bits 12-15, two's complement, 0 = padding).
+        Slots >= nslots are the constant table (copied into LDS by the kernel prologue)."""
         words, offs = [], []
         for cur in self.rounds:
             ents = []
@@ -607,9 +618,11 @@ class Program:
                 ents.append((v, a, b))
             nA = max(len(a) for _, a, _ in ents)
             nB = max(len(b) for _, _, b in ents)
+            mA = max((abs(c) for _, a, _ in ents for _, c in a), default=1)
+            mB = max((abs(c) for _, _, b in ents for _, c in b), default=1)
             stride = 1 + nA + nB
             offs.append(len(words))
-            words += [nA, nB, stride, len(ents)]
+            words += [nA | (mA << 8), nB | (mB << 8), stride, len(ents)]
             for v, a, b in ents:
                 flags = (1 << 12) if v.kind == "mul" else (1 << 13) if v.kind == "inv" else 0
                 words.append(v.slot | flags)
@@ -625,10 +638,11 @@ class Program:
         mem = {}
         for name, v in self.tr.inputs.items():
             mem[v.slot] = inputs[name] % P
-        consts = {CONST_BASE + k: c for k, c in enumerate(self.consts)}
+        consts = {self.nslots + k: c for k, c in enumerate(self.consts)}
         words, offs = self.encode()
         for r, off in enumerate(offs):
             nA, nB, stride, used = words[off:off + 4]
+            nA, nB = nA & 0xFF, nB & 0xFF
             writes = []
             for lane in range(used):
                 e = words[off + 4 + lane * stride: off + 4 + (lane + 1) * stride]
@@ -641,7 +655,7 @@ class Program:
                         if s == SLOT_NONE or c == 0:
                             continue
                         c = c - 16 if c >= 8 else c
-                        val = consts[s] if s >= CONST_BASE else mem[s]
+                        val = consts[s] if s >= self.nslots else mem[s]
                         acc = (acc + c * val) % P
                     return acc
                 A = ev(e[1:1 + nA])
@@ -729,6 +743,7 @@ def emit(progs, path):
         lines.append(f"#define LCV_PROG_{N}_ROUNDS {len(offs)}")
         lines.append(f"#define LCV_PROG_{N}_SLOTS {p.nslots}")
         lines.append(f"#define LCV_PROG_{N}_NCONST {len(p.consts)}")
+        lines.append(f"#define LCV_PROG_{N}_MAXSUM {p.max_abs_sum()}")
         for nm, s in sorted(p.state_slots.items(), key=lambda kv: kv[1]):
             lines.append(f"#define LCV_PROG_{N}_SLOT_{nm.upper()} {s}")
         lines.append(f"static const uint16_t kProg_{p.name}_words[{len(words)}] = {{")
