@@ -51,6 +51,33 @@ namespace lcv {
 
 LCV_FN uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// add / subtract with carry.  On the device clang's __builtin_addc/__builtin_subc lower to one
+// v_add_co/v_addc_co (v_sub_co/v_subb_co) per limb; 64-bit temporaries would cost ~4 instructions.
+LCV_FN uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+#if defined(__clang__)
+  unsigned co;
+  const uint32_t r = __builtin_addc(a, b, cin, &co);
+  cout = co;
+  return r;
+#else
+  const uint64_t s = (uint64_t)a + b + cin;
+  cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+#endif
+}
+LCV_FN uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+#if defined(__clang__)
+  unsigned bo;
+  const uint32_t r = __builtin_subc(a, b, bin, &bo);
+  bout = bo;
+  return r;
+#else
+  const uint64_t s = (uint64_t)a - b - bin;
+  bout = (uint32_t)(s >> 63);
+  return (uint32_t)s;
+#endif
+}
+
 LCV_FN uint32_t ld_le32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }

@@ -60,22 +60,14 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t n, uint32_t maxc, cons
     uint32_t v[12], d[12];
     LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = src[j];
     uint32_t br = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) {  // d = p - v  (in [1, p])
-      const uint64_t x = (uint64_t)PL[j] - v[j] - br;
-      d[j] = (uint32_t)x;
-      br = (uint32_t)(x >> 63);
-    }
+    LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(PL[j], v[j], br, br);  // d = p - v in [1, p]
     const uint32_t a = (uint32_t)(c < 0 ? -c : c);
     const uint32_t negm = c < 0 ? 0xFFFFFFFFu : 0u;
     LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = (d[j] & negm) | (v[j] & ~negm);
     for (uint32_t rep = 0; rep < maxc; ++rep) {
       const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;
       uint32_t cy = 0;
-      LCV_UNROLL for (int j = 0; j < 12; ++j) {
-        const uint64_t x = (uint64_t)acc[j] + (v[j] & keep) + cy;
-        acc[j] = (uint32_t)x;
-        cy = (uint32_t)(x >> 32);
-      }
+      LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], v[j] & keep, cy, cy);
       acc[12] += cy;
     }
   }
@@ -88,11 +80,7 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t n, uint32_t maxc, cons
     }
     sp[12] = cy;
     uint32_t br = 0;
-    LCV_UNROLL for (int j = 0; j < 13; ++j) {
-      const uint64_t x = (uint64_t)acc[j] - sp[j] - br;
-      d[j] = (uint32_t)x;
-      br = (uint32_t)(x >> 63);
-    }
+    LCV_UNROLL for (int j = 0; j < 13; ++j) d[j] = subc32(acc[j], sp[j], br, br);
     LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = br ? acc[j] : d[j];
   }
   LCV_UNROLL for (int j = 0; j < 12; ++j) out.v[j] = acc[j];
@@ -111,35 +99,21 @@ LCV_FN void raw_shr1(fp& a) {
 }
 LCV_FN bool raw_sub(fp& r, const fp& a, const fp& b) {  // r = a - b, returns borrow
   uint32_t br = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t s = (uint64_t)a.v[j] - b.v[j] - br;
-    r.v[j] = (uint32_t)s;
-    br = (uint32_t)(s >> 63);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = subc32(a.v[j], b.v[j], br, br);
   return br != 0;
 }
 LCV_FN void raw_half_mod(fp& x) {  // x / 2 mod p, x < p
   constexpr uint32_t PL[12] = LCV_P_INIT;
-  if (x.v[0] & 1u) {
-    uint32_t c = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) {
-      uint64_t s = (uint64_t)x.v[j] + PL[j] + c;
-      x.v[j] = (uint32_t)s;
-      c = (uint32_t)(s >> 32);
-    }
-  }
-  raw_shr1(x);
+  const uint32_t m = 0u - (x.v[0] & 1u);
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = addc32(x.v[j], PL[j] & m, c, c);
+  raw_shr1(x);  // x + p < 2^382: no bit is lost
 }
 LCV_FN void raw_sub_mod(fp& r, const fp& a, const fp& b) {  // (a - b) mod p, a, b < p
   constexpr uint32_t PL[12] = LCV_P_INIT;
-  if (raw_sub(r, a, b)) {
-    uint32_t c = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) {
-      uint64_t s = (uint64_t)r.v[j] + PL[j] + c;
-      r.v[j] = (uint32_t)s;
-      c = (uint32_t)(s >> 32);
-    }
-  }
+  const uint32_t m = raw_sub(r, a, b) ? 0xFFFFFFFFu : 0u;
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = addc32(r.v[j], PL[j] & m, c, c);
 }
 LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
   fp u, v, x1, x2, t;

@@ -39,11 +39,7 @@ LCV_FN void fp_reduce_once(uint32_t r[12], const uint32_t t[12]) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
   uint32_t d[12];
   uint32_t br = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t s = (uint64_t)t[j] - PL[j] - br;
-    d[j] = (uint32_t)s;
-    br = (uint32_t)(s >> 63);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(t[j], PL[j], br, br);
   LCV_UNROLL for (int j = 0; j < 12; ++j) r[j] = br ? t[j] : d[j];
 }
 
@@ -51,11 +47,7 @@ LCV_FN void fp_add(fp& r, const fp& a, const fp& b) {
   LCV_COUNT(1);
   uint32_t s[12];
   uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t x = (uint64_t)a.v[j] + b.v[j] + c;
-    s[j] = (uint32_t)x;
-    c = (uint32_t)(x >> 32);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) s[j] = addc32(a.v[j], b.v[j], c, c);
   fp_reduce_once(r.v, s);
 }
 
@@ -64,18 +56,10 @@ LCV_FN void fp_sub(fp& r, const fp& a, const fp& b) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
   uint32_t d[12];
   uint32_t br = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t x = (uint64_t)a.v[j] - b.v[j] - br;
-    d[j] = (uint32_t)x;
-    br = (uint32_t)(x >> 63);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(a.v[j], b.v[j], br, br);
   const uint32_t m = 0u - br;
   uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t x = (uint64_t)d[j] + (PL[j] & m) + c;
-    r.v[j] = (uint32_t)x;
-    c = (uint32_t)(x >> 32);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = addc32(d[j], PL[j] & m, c, c);
 }
 
 LCV_FN void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
@@ -90,16 +74,14 @@ LCV_FN void fp_half(fp& r, const fp& a) {
   const uint32_t m = 0u - (a.v[0] & 1u);
   uint32_t t[12];
   uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t x = (uint64_t)a.v[j] + (PL[j] & m) + c;
-    t[j] = (uint32_t)x;
-    c = (uint32_t)(x >> 32);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) t[j] = addc32(a.v[j], PL[j] & m, c, c);
   LCV_UNROLL for (int j = 0; j < 11; ++j) r.v[j] = (t[j] >> 1) | (t[j + 1] << 31);
-  r.v[11] = t[11] >> 1;
+  r.v[11] = (t[11] >> 1) | (c << 31);
 }
 
-// CIOS Montgomery multiplication, no-carry variant.  r may alias a or b.
+// CIOS Montgomery multiplication, no-carry variant.  r may alias a or b.  Each inner step is
+// v_mad_u64_u32 (a_j * b_i + t_j, exact in 64 bits) and an add-with-carry of the running carry
+// (a_j b_i + t_j + A < 2^64, so the high word absorbs the carry without overflow).
 LCV_FN void fp_mul_impl(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
   uint32_t t[12];
@@ -112,11 +94,13 @@ LCV_FN void fp_mul_impl(uint32_t r[12], const uint32_t a[12], const uint32_t b[1
     uint64_t c2 = (uint64_t)m * PL[0] + (uint32_t)c;
     uint32_t C = (uint32_t)(c2 >> 32);
     LCV_UNROLL for (int j = 1; j < 12; ++j) {
-      c = (uint64_t)a[j] * bi + t[j] + A;
-      A = (uint32_t)(c >> 32);
-      c2 = (uint64_t)m * PL[j] + (uint32_t)c + C;
-      C = (uint32_t)(c2 >> 32);
-      t[j - 1] = (uint32_t)c2;
+      c = (uint64_t)a[j] * bi + t[j];
+      uint32_t co, co2;
+      const uint32_t lo = addc32((uint32_t)c, A, 0u, co);
+      A = (uint32_t)(c >> 32) + co;
+      c2 = (uint64_t)m * PL[j] + lo;
+      t[j - 1] = addc32((uint32_t)c2, C, 0u, co2);
+      C = (uint32_t)(c2 >> 32) + co2;
     }
     t[11] = A + C;
   }
@@ -189,10 +173,7 @@ LCV_FN void fp_raw_to_be48(uint8_t* p, const fp& r) {
 // a < b on raw limbs
 LCV_FN bool fp_raw_lt(const fp& a, const fp& b) {
   uint32_t br = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) {
-    uint64_t s = (uint64_t)a.v[j] - b.v[j] - br;
-    br = (uint32_t)(s >> 63);
-  }
+  LCV_UNROLL for (int j = 0; j < 12; ++j) (void)subc32(a.v[j], b.v[j], br, br);
   return br != 0;
 }
 LCV_FN bool fp_raw_lt_p(const fp& a) {
