@@ -11,7 +11,7 @@
 //
 // Encoding (uint16): round header [nA, nB, stride, used], then `used` entries of `stride` words:
 //   dst | 0x1000 (MUL) | 0x2000 (INV),  nA terms,  nB terms;   term = slot | coef << 12 (4-bit signed)
-// (header words 0/1 carry the round's max |coef| of A/B in bits 8..15; slots >= nslots are constants)
+// (header words 0/1: n | max|coef| << 8 | reduction bits << 11 | full << 14; slots >= nslots are constants)
 #pragma once
 #include "lcv_items.hpp"
 
@@ -41,13 +41,16 @@ LCV_FN void eng_store(uint32_t* lds, uint32_t slot, const fp& v) {
   LCV_UNROLL for (int k = 0; k < 12; ++k) dst[k] = v.v[k];
 }
 
-// out = (sum_k c_k * value(slot_k)) mod p.  Branch-free and uniform across the wave: n (terms) and
-// maxc (largest |c| in the round) come from the round header; padding terms have c = 0.  Each term
-// adds |c| copies of v (c > 0) or of p - v (c < 0) into an UNREDUCED 13-limb accumulator
-// (< MAXSUM * p < 2^387, MAXSUM from the generator), reduced once at the end by conditional
-// subtraction of 32p, 16p, ..., p.
-LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t n, uint32_t maxc, const uint32_t* lds) {
+// out = sum_k c_k * value(slot_k) (mod p).  Branch-free and uniform across the wave: the round
+// header h gives n (terms), maxc (largest |c| in the round), k (2^k > sum |c|) and whether the
+// result must be fully reduced (< p, LIN results are stored) or only <= 2p (a Montgomery operand:
+// a, b <= 2p gives ab < R p and a result < 2p).  Each term adds |c| * v (c > 0) or |c| * (p - v)
+// (c < 0, p - v in [1, p]) into an UNREDUCED 13-limb accumulator (< 2^k p <= 2^6 p), then
+// conditional subtraction of 2^s p for s = k-1 .. (full ? 0 : 1).  |c| * v: masked repeated
+// addition when maxc <= 2, else a v_mad_u64_u32 chain (cost independent of |c|).
+LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
+  const uint32_t n = h & 0xFFu, maxc = (h >> 8) & 7u, kb = (h >> 11) & 7u, lo = (h >> 14) & 1u ? 0u : 1u;
   uint32_t acc[13];
   LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = 0;
   for (uint32_t k = 0; k < n; ++k) {
@@ -64,14 +67,24 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t n, uint32_t maxc, cons
     const uint32_t a = (uint32_t)(c < 0 ? -c : c);
     const uint32_t negm = c < 0 ? 0xFFFFFFFFu : 0u;
     LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = (d[j] & negm) | (v[j] & ~negm);
-    for (uint32_t rep = 0; rep < maxc; ++rep) {
-      const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;
-      uint32_t cy = 0;
-      LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], v[j] & keep, cy, cy);
-      acc[12] += cy;
+    if (maxc <= 2) {
+      for (uint32_t rep = 0; rep < maxc; ++rep) {
+        const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;
+        uint32_t cy = 0;
+        LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], v[j] & keep, cy, cy);
+        acc[12] += cy;
+      }
+    } else {
+      uint32_t hi = 0, cy = 0;
+      LCV_UNROLL for (int j = 0; j < 12; ++j) {
+        const uint64_t pr = (uint64_t)v[j] * a + hi;  // < 2^35: one v_mad_u64_u32
+        hi = (uint32_t)(pr >> 32);
+        acc[j] = addc32(acc[j], (uint32_t)pr, cy, cy);
+      }
+      acc[12] += hi + cy;
     }
   }
-  LCV_UNROLL for (int s = 5; s >= 0; --s) {  // acc < 64 p  ->  acc mod p
+  for (uint32_t s = kb; s-- > lo;) {  // acc < 2^kb p  ->  acc < 2^lo p
     uint32_t sp[13], d[13];
     uint32_t cy = 0;
     LCV_UNROLL for (int j = 0; j < 12; ++j) {  // sp = p << s
@@ -150,15 +163,15 @@ LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
 LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds) {
   const uint16_t* rp = P.words + P.offs[r];
   const uint32_t hA = rp[0], hB = rp[1], stride = rp[2], used = rp[3];
-  const uint32_t nA = hA & 0xFFu, nB = hB & 0xFFu;
+  const uint32_t nA = hA & 0xFFu;
   if (lane >= used) return;
   const uint16_t* e = rp + 4 + lane * stride;
   const uint32_t dst = e[0];
   fp a;
-  eng_eval(a, e + 1, nA, hA >> 8, lds);
+  eng_eval(a, e + 1, hA, lds);
   if (dst & ENG_MUL) {
     fp b;
-    eng_eval(b, e + 1 + nA, nB, hB >> 8, lds);
+    eng_eval(b, e + 1 + nA, hB, lds);
     fp_mul(a, a, b);
   } else if (dst & ENG_INV) {
     fp_inv_bingcd(a, a);
@@ -180,33 +193,39 @@ LCV_FN uint32_t fp12_soa_slot(uint32_t g) { return (g & 1u) ? 3u + (g >> 1) : (g
 // Miller loop of both pairings.  Prologue (lane k < 12 loads input k): Q1 = H(m), Q2 = signature,
 // P1 = aggregate pubkey, P2 = -G1; an identity Q_k becomes (Q_k = G2 generator, P_k = (0, 0)), whose
 // lines are Fp2 constants killed by the final exponentiation (e(P, O) = 1).  Epilogue: f -> W.f.
+// out of line: keeps the prologue's constants (G2 generator, -G1) from being hoisted into registers
+// that would stay live across the whole round loop
+LCV_OUTLINE void miller_prologue(uint32_t i, uint32_t lane, uint32_t* lds, const Work& W) {
+  if (lane >= 12) return;
+  const bool q1_id = W.qh_inf[i] != 0, q2_id = W.sig_status[i] != PT_OK;
+  fp v;
+  if (lane < 8) {
+    const bool id = lane < 4 ? q1_id : q2_id;
+    const uint32_t k = lane & 3u;
+    if (id) {
+      fp2 g;
+      if (k < 2) LCV_FP2_SET(g, LCV_G2X);
+      else LCV_FP2_SET(g, LCV_G2Y);
+      v = (k & 1u) ? g.c1 : g.c0;
+    } else {
+      soa_ld_fp(v, lane < 4 ? W.qh : W.qs, W.cap, i, k);
+    }
+  } else if (lane < 10) {  // P1 = (-x, y) of the aggregate pubkey
+    soa_ld_fp(v, W.pk, W.cap, i, lane - 8);
+    if (lane == 8) fp_neg(v, v);
+    if (q1_id) fp_zero(v);
+  } else {                 // P2 = -G1: (-x, y) = (-G1x, -G1y)
+    if (lane == 10) { LCV_FP_SET(v, LCV_G1X_INIT); fp_neg(v, v); }
+    else LCV_FP_SET(v, LCV_G1NEGY_INIT);
+    if (q2_id) fp_zero(v);
+  }
+  eng_store(lds, lane, v);  // input slots 0..11 in the order of LCV_PROG_MILLER_SLOT_*
+}
+
 LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
   if (r == 0) {
     eng_load_consts(P, lane, LCV_PROG_MILLER_TEAM, lds);
-    if (lane >= 12) return;
-    const bool q1_id = W.qh_inf[i] != 0, q2_id = W.sig_status[i] != PT_OK;
-    fp v;
-    if (lane < 8) {
-      const bool id = lane < 4 ? q1_id : q2_id;
-      const uint32_t k = lane & 3u;
-      if (id) {
-        fp2 g;
-        if (k < 2) LCV_FP2_SET(g, LCV_G2X);
-        else LCV_FP2_SET(g, LCV_G2Y);
-        v = (k & 1u) ? g.c1 : g.c0;
-      } else {
-        soa_ld_fp(v, lane < 4 ? W.qh : W.qs, W.cap, i, k);
-      }
-    } else if (lane < 10) {  // P1 = (-x, y) of the aggregate pubkey
-      soa_ld_fp(v, W.pk, W.cap, i, lane - 8);
-      if (lane == 8) fp_neg(v, v);
-      if (q1_id) fp_zero(v);
-    } else {                 // P2 = -G1: (-x, y) = (-G1x, -G1y)
-      if (lane == 10) { LCV_FP_SET(v, LCV_G1X_INIT); fp_neg(v, v); }
-      else LCV_FP_SET(v, LCV_G1NEGY_INIT);
-      if (q2_id) fp_zero(v);
-    }
-    eng_store(lds, lane, v);  // input slots 0..11 in the order of LCV_PROG_MILLER_SLOT_*
+    miller_prologue(i, lane, lds, W);
   } else if (r <= P.rounds) {
     eng_round(P, r - 1, lane, lds);
   } else if (lane < 12) {

@@ -25,7 +25,7 @@ template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t
 // through F::LDS_WORDS words of LDS per item; the item's work is f.rounds() rounds separated by
 // barriers (every lane of a team reads what the previous rounds wrote).
 template <class F>
-__global__ __launch_bounds__(64, 1) void k_team(F f, uint32_t n) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(168))) void k_team(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
   __shared__ uint32_t lds[G * F::LDS_WORDS];
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;

@@ -605,7 +605,8 @@ class Program:
 
     # ---------------------------------------------------------------- encoding
     def encode(self):
-        """uint16 words.  Round r at offs[r]: [nA | maxcA << 8, nB | maxcB << 8, stride, used] then `used`
+        """uint16 words.  Round r at offs[r]: [hA, hB, stride, used], h = n | maxc << 8 | k << 11 |
+        full << 14 (n terms, max |coef|, reduction bits k, full reduction), then `used`
         lane entries of `stride` words: dst | flags, nA terms, nB terms.  dst bits 0-11 slot, bit 12
         MUL, bit 13 INV.  term = slot (bits 0-11) | coef (bits 12-15, two's complement, 0 = padding).
         Slots >= nslots are the constant table (copied into LDS by the kernel prologue)."""
@@ -620,9 +621,19 @@ class Program:
             nB = max(len(b) for _, _, b in ents)
             mA = max((abs(c) for _, a, _ in ents for _, c in a), default=1)
             mB = max((abs(c) for _, _, b in ents for _, c in b), default=1)
+            # reduction of the unreduced accumulator (< S p, S = sum |c|): conditional subtraction of
+            # 2^s p for s = k-1 .. lo with 2^k > S; lo = 0 (< p: LIN results are stored) or 1
+            # (<= 2p suffices for a Montgomery operand: a, b <= 2p -> ab < R p)
+            def kbits(S):
+                return S.bit_length()  # smallest k with 2^k > S
+            kA = max(kbits(sum(abs(c) for _, c in a)) for _, a, _ in ents)
+            fullA = any(v.kind != "mul" for v, _, _ in ents)
+            kB = max((kbits(sum(abs(c) for _, c in b)) for v, _, b in ents if v.kind == "mul"), default=0)
+            assert kA <= 6 and kB <= 6 and mA <= 7 and mB <= 7
             stride = 1 + nA + nB
             offs.append(len(words))
-            words += [nA | (mA << 8), nB | (mB << 8), stride, len(ents)]
+            words += [nA | (mA << 8) | (kA << 11) | ((1 if fullA else 0) << 14),
+                      nB | (mB << 8) | (kB << 11), stride, len(ents)]
             for v, a, b in ents:
                 flags = (1 << 12) if v.kind == "mul" else (1 << 13) if v.kind == "inv" else 0
                 words.append(v.slot | flags)
@@ -642,7 +653,7 @@ class Program:
         words, offs = self.encode()
         for r, off in enumerate(offs):
             nA, nB, stride, used = words[off:off + 4]
-            nA, nB = nA & 0xFF, nB & 0xFF
+            nA, nB = nA & 0xFF, nB & 0xFF  # (bits 8+: coefficient / reduction metadata)
             writes = []
             for lane in range(used):
                 e = words[off + 4 + lane * stride: off + 4 + (lane + 1) * stride]
