@@ -99,66 +99,6 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds
   LCV_UNROLL for (int j = 0; j < 12; ++j) out.v[j] = acc[j];
 }
 
-// Variable-time binary extended Euclid on canonical values: r = a^-1 mod p (0 -> 0).  Verification
-// handles public data only, so variable time is acceptable; it is ~10x fewer cycles than a^(p-2).
-LCV_FN bool raw_is_one(const fp& a) {
-  uint32_t x = a.v[0] ^ 1u;
-  LCV_UNROLL for (int i = 1; i < 12; ++i) x |= a.v[i];
-  return x == 0;
-}
-LCV_FN void raw_shr1(fp& a) {
-  LCV_UNROLL for (int j = 0; j < 11; ++j) a.v[j] = (a.v[j] >> 1) | (a.v[j + 1] << 31);
-  a.v[11] >>= 1;
-}
-LCV_FN bool raw_sub(fp& r, const fp& a, const fp& b) {  // r = a - b, returns borrow
-  uint32_t br = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = subc32(a.v[j], b.v[j], br, br);
-  return br != 0;
-}
-LCV_FN void raw_half_mod(fp& x) {  // x / 2 mod p, x < p
-  constexpr uint32_t PL[12] = LCV_P_INIT;
-  const uint32_t m = 0u - (x.v[0] & 1u);
-  uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = addc32(x.v[j], PL[j] & m, c, c);
-  raw_shr1(x);  // x + p < 2^382: no bit is lost
-}
-LCV_FN void raw_sub_mod(fp& r, const fp& a, const fp& b) {  // (a - b) mod p, a, b < p
-  constexpr uint32_t PL[12] = LCV_P_INIT;
-  const uint32_t m = raw_sub(r, a, b) ? 0xFFFFFFFFu : 0u;
-  uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = addc32(r.v[j], PL[j] & m, c, c);
-}
-LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
-  fp u, v, x1, x2, t;
-  fp_from_mont(u, a_mont);
-  if (fp_is_zero(u)) {
-    fp_zero(r);
-    return;
-  }
-  LCV_FP_SET(v, LCV_P_INIT);
-  fp_zero(x1);
-  x1.v[0] = 1;
-  fp_zero(x2);
-  while (!raw_is_one(u) && !raw_is_one(v)) {
-    while ((u.v[0] & 1u) == 0) {
-      raw_shr1(u);
-      raw_half_mod(x1);
-    }
-    while ((v.v[0] & 1u) == 0) {
-      raw_shr1(v);
-      raw_half_mod(x2);
-    }
-    if (!raw_sub(t, u, v)) {  // u >= v
-      u = t;
-      raw_sub_mod(x1, x1, x2);
-    } else {
-      raw_sub(v, v, u);
-      raw_sub_mod(x2, x2, x1);
-    }
-  }
-  fp_to_mont(r, raw_is_one(u) ? x1 : x2);
-}
-
 // one round of a program for lane `lane` of the team whose LDS slots start at `lds`
 LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds) {
   const uint16_t* rp = P.words + P.offs[r];
@@ -260,6 +200,56 @@ LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds,
       }
       W.pair_ok[i] = ok ? 1 : 0;
     }
+  }
+}
+
+// hash_to_G2 tail: isogeny of both SSWU points, addition, cofactor clearing, affine H(m) -> W.qh
+LCV_FN void item_h2c_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+  if (r == 0) {
+    eng_load_consts(P, lane, LCV_PROG_H2C_TEAM, lds);
+    for (uint32_t k = lane; k < 8; k += LCV_PROG_H2C_TEAM) {
+      fp v;
+      soa_ld_fp(v, W.qmap, W.cap, i, k);
+      eng_store(lds, LCV_PROG_H2C_SLOT_M0X0 + k, v);
+    }
+  } else if (r <= P.rounds) {
+    eng_round(P, r - 1, lane, lds);
+  } else if (lane < 4) {
+    fp v;
+    eng_load(v, lds, LCV_PROG_H2C_SLOT_HX0 + lane);
+    soa_st_fp(W.qh, W.cap, i, lane, v);
+    if (lane == 0) {
+      fp z0, z1;
+      eng_load(z0, lds, LCV_PROG_H2C_SLOT_HZ0);
+      eng_load(z1, lds, LCV_PROG_H2C_SLOT_HZ0 + 1);
+      W.qh_inf[i] = (fp_is_zero(z0) && fp_is_zero(z1)) ? 1 : 0;
+    }
+  }
+}
+
+// G2 subgroup check of the decoded signature (psi(P) == [x]P); a failure turns PT_OK into PT_BAD
+LCV_FN void item_g2sub_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+  if (r == 0) {
+    eng_load_consts(P, lane, LCV_PROG_G2SUB_TEAM, lds);
+    for (uint32_t k = lane; k < 4; k += LCV_PROG_G2SUB_TEAM) {
+      fp v;
+      soa_ld_fp(v, W.qs, W.cap, i, k);
+      eng_store(lds, LCV_PROG_G2SUB_SLOT_SX0 + k, v);
+    }
+  } else if (r <= P.rounds) {
+    eng_round(P, r - 1, lane, lds);
+  } else if (lane == 0 && W.sig_status[i] == PT_OK) {
+    bool e_zero = true;
+    for (uint32_t k = 0; k < 4; ++k) {
+      fp v;
+      eng_load(v, lds, LCV_PROG_G2SUB_SLOT_E10 + k);
+      e_zero = e_zero && fp_is_zero(v);
+    }
+    fp z0, z1;
+    eng_load(z0, lds, LCV_PROG_G2SUB_SLOT_Z0);
+    eng_load(z1, lds, LCV_PROG_G2SUB_SLOT_Z0 + 1);
+    const bool z_zero = fp_is_zero(z0) && fp_is_zero(z1);
+    if (!e_zero || z_zero) W.sig_status[i] = PT_BAD;
   }
 }
 

@@ -147,7 +147,7 @@ LCV_FN void fp_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }
     }                                                                      \
     r = acc;                                                               \
   }
-LCV_DEF_POW(fp_inv, LCV_EXP_P_MINUS_2, LCV_EXP_P_MINUS_2_BITS)           // a^(p-2) (inv0: 0 -> 0)
+LCV_DEF_POW(fp_inv_fermat, LCV_EXP_P_MINUS_2, LCV_EXP_P_MINUS_2_BITS)    // a^(p-2) (inv0: 0 -> 0)
 LCV_DEF_POW(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
 LCV_DEF_POW(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
 LCV_DEF_POW(fp_pow_pm1d2, LCV_EXP_P_MINUS_1_DIV_2, LCV_EXP_P_MINUS_1_DIV_2_BITS)  // Legendre
@@ -198,6 +198,69 @@ LCV_FN void fp_from_be48_mont(fp& r, const uint8_t* p) {  // caller guarantees v
   fp_raw_from_be48(raw, p);
   fp_to_mont(r, raw);
 }
+
+// Variable-time binary extended Euclid on canonical values: r = a^-1 mod p (0 -> 0).  Verification
+// handles public data only, so variable time is acceptable; it is ~10x fewer cycles than a^(p-2).
+LCV_FN bool raw_is_one(const fp& a) {
+  uint32_t x = a.v[0] ^ 1u;
+  LCV_UNROLL for (int i = 1; i < 12; ++i) x |= a.v[i];
+  return x == 0;
+}
+LCV_FN void raw_shr1(fp& a) {
+  LCV_UNROLL for (int j = 0; j < 11; ++j) a.v[j] = (a.v[j] >> 1) | (a.v[j + 1] << 31);
+  a.v[11] >>= 1;
+}
+LCV_FN bool raw_sub(fp& r, const fp& a, const fp& b) {  // r = a - b, returns borrow
+  uint32_t br = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = subc32(a.v[j], b.v[j], br, br);
+  return br != 0;
+}
+LCV_FN void raw_half_mod(fp& x) {  // x / 2 mod p, x < p
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  const uint32_t m = 0u - (x.v[0] & 1u);
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = addc32(x.v[j], PL[j] & m, c, c);
+  raw_shr1(x);  // x + p < 2^382: no bit is lost
+}
+LCV_FN void raw_sub_mod(fp& r, const fp& a, const fp& b) {  // (a - b) mod p, a, b < p
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  const uint32_t m = raw_sub(r, a, b) ? 0xFFFFFFFFu : 0u;
+  uint32_t c = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = addc32(r.v[j], PL[j] & m, c, c);
+}
+LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
+  fp u, v, x1, x2, t;
+  fp_from_mont(u, a_mont);
+  if (fp_is_zero(u)) {
+    fp_zero(r);
+    return;
+  }
+  LCV_FP_SET(v, LCV_P_INIT);
+  fp_zero(x1);
+  x1.v[0] = 1;
+  fp_zero(x2);
+  while (!raw_is_one(u) && !raw_is_one(v)) {
+    while ((u.v[0] & 1u) == 0) {
+      raw_shr1(u);
+      raw_half_mod(x1);
+    }
+    while ((v.v[0] & 1u) == 0) {
+      raw_shr1(v);
+      raw_half_mod(x2);
+    }
+    if (!raw_sub(t, u, v)) {  // u >= v
+      u = t;
+      raw_sub_mod(x1, x1, x2);
+    } else {
+      raw_sub(v, v, u);
+      raw_sub_mod(x2, x2, x1);
+    }
+  }
+  fp_to_mont(r, raw_is_one(u) ? x1 : x2);
+}
+
+// Fp inversion (inv0: 0 -> 0) for every stage: the binary algorithm above
+LCV_FN void fp_inv(fp& r, const fp& a) { fp_inv_bingcd(r, a); }
 
 // ============================================================================ Fp2
 LCV_FN void fp2_zero(fp2& r) { fp_zero(r.c0); fp_zero(r.c1); }

@@ -17,3 +17,15 @@ struct F_eng_fexp {
   LCV_HD uint32_t rounds() const { return P.rounds + 2; }
   LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_fexp_team(i, lane, r, lds, P, W); }
 };
+struct F_eng_h2c {
+  Work W; ProgView P;
+  static constexpr uint32_t TEAM = LCV_PROG_H2C_TEAM, LDS_WORDS = (LCV_PROG_H2C_SLOTS + LCV_PROG_H2C_NCONST) * 12;
+  LCV_HD uint32_t rounds() const { return P.rounds + 2; }
+  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_h2c_team(i, lane, r, lds, P, W); }
+};
+struct F_eng_g2sub {
+  Work W; ProgView P;
+  static constexpr uint32_t TEAM = LCV_PROG_G2SUB_TEAM, LDS_WORDS = (LCV_PROG_G2SUB_SLOTS + LCV_PROG_G2SUB_NCONST) * 12;
+  LCV_HD uint32_t rounds() const { return P.rounds + 2; }
+  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds) const { item_g2sub_team(i, lane, r, lds, P, W); }
+};

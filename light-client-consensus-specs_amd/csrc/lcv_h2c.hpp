@@ -82,8 +82,8 @@ LCV_FN void iso_map_g2(g2j& r, const fp2& x, const fp2& y) {
   fp2_mul(r.y, t, y);
 }
 
-// simplified SWU (RFC 9380 §6.6.2, straight-line form) then the isogeny
-LCV_FN void map_to_curve_g2(g2j& r, const fp2& u) {
+// simplified SWU onto E2' (RFC 9380 §6.6.2, straight-line form): affine (x, y) on E2'
+LCV_FN void sswu_e2prime(fp2& xo, fp2& yo, const fp2& u) {
   fp2 A, B, Z, t, u2, zu2, den, x1, gx1, x2, gx2, x, gx, y, one, c;
   LCV_FP2_SET(A, LCV_ISO_A);
   LCV_FP2_SET(B, LCV_ISO_B);
@@ -122,7 +122,33 @@ LCV_FN void map_to_curve_g2(g2j& r, const fp2& u) {
   }
   fp2_sqrt_alpha(y, gx, alpha);
   if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
+  xo = x;
+  yo = y;
+}
+
+
+// map_to_curve = SSWU then the 3-isogeny (used by the signer; verification runs the isogeny and the
+// cofactor clearing as the team program `h2c`, lcv_engine.hpp)
+LCV_FN void map_to_curve_g2(g2j& r, const fp2& u) {
+  fp2 x, y;
+  sswu_e2prime(x, y, u);
   iso_map_g2(r, x, y);
+}
+
+// hash_to_field(msg, 2)[m] (RFC 9380 §5.2; u_1 needs the xmd chain through u_0's blocks)
+LCV_FN void hash_to_field_u(fp2& u, const h256& msg, uint32_t m) {
+  h256 b0, prev, hi, lo;
+  xmd_b0(b0, msg);
+  h256_zero(prev);
+  LCV_NOUNROLL for (uint32_t k = 0; k <= m; ++k) {
+    xmd_next(hi, b0, prev, 4 * k + 1);
+    xmd_next(lo, b0, hi, 4 * k + 2);
+    fp_from_xmd64(u.c0, hi, lo);
+    xmd_next(hi, b0, lo, 4 * k + 3);
+    xmd_next(lo, b0, hi, 4 * k + 4);
+    fp_from_xmd64(u.c1, hi, lo);
+    prev = lo;
+  }
 }
 
 // H(m) in G2 (Jacobian) for a 32-byte message given as 8 big-endian words

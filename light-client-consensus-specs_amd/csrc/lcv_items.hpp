@@ -9,8 +9,8 @@
 // Stage map onto the reference's validate_light_client_update (sync-protocol.md:386-465):
 //   item_nsc_team   hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449)
 //   item_pre        every non-BLS assert (:392-449) + signing root (:460-463) -> first failing reason
-//   item_h2c        hash_to_G2(signing_root)                   -+
-//   item_sig        signature decode + subgroup check           |  bls.FastAggregateVerify (:464)
+//   item_h2c_map + h2c program   hash_to_G2(signing_root)       -+
+//   item_sig + g2sub program     signature decode + subgroup     |  bls.FastAggregateVerify (:464)
 //   item_agg        masked G1 aggregation of participant keys   |
 //   item_miller_team / item_fexp_team (lcv_engine.hpp)  pairing  -+
 //   item_verdict    conjunction + reason code
@@ -65,6 +65,7 @@ struct Work {
   uint32_t* comm_id;     // [cap] committee used for the signature (0 current, 1 next)
   uint32_t* nsc_root;    // [8][pool_cap]
   uint8_t* nsc_flags;    // [pool_cap] bit0: all-zero, bit1: equals store.next_sync_committee
+  uint32_t* qmap;        // [96][cap] the two SSWU outputs on E2' (affine, 8 Fp: x0,x1,y0,y1 per map)
   uint32_t* qh;          // [48][cap] H(m) affine (x0,x1,y0,y1)
   uint8_t* qh_inf;       // [cap]
   uint32_t* qs;          // [48][cap] signature affine
@@ -250,24 +251,27 @@ LCV_FN void ld_g2a(g2a& q, const uint32_t* base, size_t cap, size_t i) {
   soa_ld_fp2(q.y, base, cap, i, 1);
 }
 
-LCV_FN void item_h2c(uint32_t i, const Work& W) {
+// hash_to_field + simplified SWU for u_m of update i (item t: i = t >> 1, m = t & 1): the serial part
+// of hash_to_G2 (two Fp exponentiations for the square root), two lanes per update; the isogeny,
+// addition and cofactor clearing run as the team program `h2c` (lcv_engine.hpp)
+LCV_FN void item_h2c_map(uint32_t t, const Work& W) {
+  const uint32_t i = t >> 1, m = t & 1u;
   h256 msg;
   soa_ld_h256(msg, W.msg, W.cap, i);
-  g2j q;
-  hash_to_g2(q, msg);
-  const bool inf = jac_is_inf(q);
-  g2a a;
-  jac_to_aff(a, q);
-  st_g2a(W.qh, W.cap, i, a);
-  W.qh_inf[i] = inf ? 1 : 0;
+  fp2 u, x, y;
+  hash_to_field_u(u, msg, m);
+  sswu_e2prime(x, y, u);
+  soa_st_fp2(W.qmap, W.cap, i, 2 * m, x);
+  soa_st_fp2(W.qmap, W.cap, i, 2 * m + 1, y);
 }
 
+// signature decode (flags, x < p, on-curve square root); the G2 subgroup check runs as the team
+// program `g2sub` (lcv_engine.hpp) and may then downgrade PT_OK to PT_BAD
 LCV_FN void item_sig(uint32_t i, const BatchDev& B, const Work& W) {
   g2a s;
   fp2_zero(s.x);
   fp2_zero(s.y);
-  int st = g2_decompress(s, B.sig + 96 * (size_t)i);
-  if (st == PT_OK && !g2_in_subgroup(s)) st = PT_BAD;
+  const int st = g2_decompress(s, B.sig + 96 * (size_t)i);
   st_g2a(W.qs, W.cap, i, s);
   W.sig_status[i] = (uint8_t)st;
 }
