@@ -27,9 +27,10 @@ struct ProgView {
   uint32_t nslots, nconst;
 };
 
-// prologue helper: the team copies the program's constants into its LDS slots [nslots, nslots+nconst)
-LCV_FN void eng_load_consts(const ProgView& P, uint32_t lane, uint32_t team, uint32_t* lds) {
-  for (uint32_t k = lane; k < 12 * P.nconst; k += team) lds[12 * P.nslots + k] = P.consts[k];
+// prologue helper: the program's constants go to the block's shared LDS region `cl` (slot nslots + k
+// is constant k); every team writes the same values, the round barrier publishes them
+LCV_FN void eng_load_consts(const ProgView& P, uint32_t lane, uint32_t team, uint32_t* cl) {
+  for (uint32_t k = lane; k < 12 * P.nconst; k += team) cl[k] = P.consts[k];
 }
 
 LCV_FN void eng_load(fp& v, const uint32_t* lds, uint32_t slot) {
@@ -48,7 +49,7 @@ LCV_FN void eng_store(uint32_t* lds, uint32_t slot, const fp& v) {
 // (c < 0, p - v in [1, p]) into an UNREDUCED 13-limb accumulator (< 2^k p <= 2^6 p), then
 // conditional subtraction of 2^s p for s = k-1 .. (full ? 0 : 1).  |c| * v: masked repeated
 // addition when maxc <= 2, else a v_mad_u64_u32 chain (cost independent of |c|).
-LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds) {
+LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds, const uint32_t* cl, uint32_t ns) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
   const uint32_t n = h & 0xFFu, maxc = (h >> 8) & 7u, kb = (h >> 11) & 7u, lo = (h >> 14) & 1u ? 0u : 1u;
   uint32_t acc[13];
@@ -59,7 +60,7 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds
     int c = (int)(w >> 12);
     if (c >= 8) c -= 16;
     if (slot == ENG_SLOT_NONE) { slot = 0; c = 0; }
-    const uint32_t* src = lds + 12 * slot;
+    const uint32_t* src = slot >= ns ? cl + 12 * (slot - ns) : lds + 12 * slot;
     uint32_t v[12], d[12];
     LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = src[j];
     uint32_t br = 0;
@@ -100,7 +101,7 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds
 }
 
 // one round of a program for lane `lane` of the team whose LDS slots start at `lds`
-LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds) {
+LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds, const uint32_t* cl) {
   const uint16_t* rp = P.words + P.offs[r];
   const uint32_t hA = rp[0], hB = rp[1], stride = rp[2], used = rp[3];
   const uint32_t nA = hA & 0xFFu;
@@ -108,10 +109,10 @@ LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* ld
   const uint16_t* e = rp + 4 + lane * stride;
   const uint32_t dst = e[0];
   fp a;
-  eng_eval(a, e + 1, hA, lds);
+  eng_eval(a, e + 1, hA, lds, cl, P.nslots);
   if (dst & ENG_MUL) {
     fp b;
-    eng_eval(b, e + 1 + nA, hB, lds);
+    eng_eval(b, e + 1 + nA, hB, lds, cl, P.nslots);
     fp_mul(a, a, b);
   } else if (dst & ENG_INV) {
     fp_inv_bingcd(a, a);
@@ -162,12 +163,12 @@ LCV_OUTLINE void miller_prologue(uint32_t i, uint32_t lane, uint32_t* lds, const
   eng_store(lds, lane, v);  // input slots 0..11 in the order of LCV_PROG_MILLER_SLOT_*
 }
 
-LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t* cl, const ProgView& P, const Work& W) {
   if (r == 0) {
-    eng_load_consts(P, lane, LCV_PROG_MILLER_TEAM, lds);
+    eng_load_consts(P, lane, LCV_PROG_MILLER_TEAM, cl);
     miller_prologue(i, lane, lds, W);
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds);
+    eng_round(P, r - 1, lane, lds, cl);
   } else if (lane < 12) {
     fp v;
     eng_load(v, lds, LCV_PROG_MILLER_SLOT_F0_0 + lane);
@@ -176,15 +177,15 @@ LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* ld
 }
 
 // Final exponentiation; epilogue stores the pairing value (e^3) and the "== 1" verdict.
-LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t* cl, const ProgView& P, const Work& W) {
   if (r == 0) {
-    eng_load_consts(P, lane, LCV_PROG_FEXP_TEAM, lds);
+    eng_load_consts(P, lane, LCV_PROG_FEXP_TEAM, cl);
     if (lane >= 12) return;
     fp v;
     soa_ld_fp(v, W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u));
     eng_store(lds, LCV_PROG_FEXP_SLOT_F0_0 + lane, v);
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds);
+    eng_round(P, r - 1, lane, lds, cl);
   } else if (lane < 12) {
     fp v;
     eng_load(v, lds, LCV_PROG_FEXP_SLOT_R0_0 + lane);
@@ -204,16 +205,16 @@ LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds,
 }
 
 // hash_to_G2 tail: isogeny of both SSWU points, addition, cofactor clearing, affine H(m) -> W.qh
-LCV_FN void item_h2c_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+LCV_FN void item_h2c_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t* cl, const ProgView& P, const Work& W) {
   if (r == 0) {
-    eng_load_consts(P, lane, LCV_PROG_H2C_TEAM, lds);
+    eng_load_consts(P, lane, LCV_PROG_H2C_TEAM, cl);
     for (uint32_t k = lane; k < 8; k += LCV_PROG_H2C_TEAM) {
       fp v;
       soa_ld_fp(v, W.qmap, W.cap, i, k);
       eng_store(lds, LCV_PROG_H2C_SLOT_M0X0 + k, v);
     }
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds);
+    eng_round(P, r - 1, lane, lds, cl);
   } else if (lane < 4) {
     fp v;
     eng_load(v, lds, LCV_PROG_H2C_SLOT_HX0 + lane);
@@ -228,16 +229,16 @@ LCV_FN void item_h2c_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, 
 }
 
 // G2 subgroup check of the decoded signature (psi(P) == [x]P); a failure turns PT_OK into PT_BAD
-LCV_FN void item_g2sub_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const ProgView& P, const Work& W) {
+LCV_FN void item_g2sub_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t* cl, const ProgView& P, const Work& W) {
   if (r == 0) {
-    eng_load_consts(P, lane, LCV_PROG_G2SUB_TEAM, lds);
+    eng_load_consts(P, lane, LCV_PROG_G2SUB_TEAM, cl);
     for (uint32_t k = lane; k < 4; k += LCV_PROG_G2SUB_TEAM) {
       fp v;
       soa_ld_fp(v, W.qs, W.cap, i, k);
       eng_store(lds, LCV_PROG_G2SUB_SLOT_SX0 + k, v);
     }
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds);
+    eng_round(P, r - 1, lane, lds, cl);
   } else if (lane == 0 && W.sig_status[i] == PT_OK) {
     bool e_zero = true;
     for (uint32_t k = 0; k < 4; ++k) {

@@ -8,9 +8,9 @@ using namespace lcv;
 
 struct F_nsc_team {
   BatchDev B; CommitteeDev C; Work W;
-  static constexpr uint32_t TEAM = NSC_TEAM, LDS_WORDS = NSC_LDS;
+  static constexpr uint32_t TEAM = NSC_TEAM, LDS_WORDS = NSC_LDS, SHARED_WORDS = 0;
   LCV_HD uint32_t rounds() const { return NSC_ROUNDS; }
-  LCV_HD void operator()(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds) const { item_nsc_team(j, lane, r, lds, B, C, W); }
+  LCV_HD void operator()(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t*) const { item_nsc_team(j, lane, r, lds, B, C, W); }
 };
 struct F_pre { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_pre(i, B, C, P, W); } };
 struct F_h2c_map { Work W; LCV_HD void operator()(uint32_t t) const { item_h2c_map(t, W); } };

@@ -71,10 +71,10 @@ template <class F> static int be_launch(lcv_ctx*, const F& f, uint32_t n) {
 template <class F> static int be_launch_team(lcv_ctx*, const F& f, uint32_t n) {
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t i = 0; i < (int64_t)n; ++i) {
-    std::vector<uint32_t> lds(F::LDS_WORDS, 0u);
+    std::vector<uint32_t> lds(F::LDS_WORDS, 0u), shared(F::SHARED_WORDS + 1, 0u);
     const uint32_t R = f.rounds();
     for (uint32_t r = 0; r < R; ++r)
-      for (uint32_t lane = 0; lane < F::TEAM; ++lane) f((uint32_t)i, lane, r, lds.data());
+      for (uint32_t lane = 0; lane < F::TEAM; ++lane) f((uint32_t)i, lane, r, lds.data(), shared.data());
   }
   return LCV_OK;
 }

@@ -22,19 +22,19 @@ template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t
   return hipGetLastError();
 }
 // Team kernels: F::TEAM lanes cooperate on one item (64 / TEAM items per wave), exchanging values
-// through F::LDS_WORDS words of LDS per item; the item's work is f.rounds() rounds separated by
+// through F::LDS_WORDS words of LDS per item (plus F::SHARED_WORDS shared by the block's teams); the item's work is f.rounds() rounds separated by
 // barriers (every lane of a team reads what the previous rounds wrote).
 template <class F>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(168))) void k_team(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
-  __shared__ uint32_t lds[G * F::LDS_WORDS];
+  __shared__ uint32_t lds[F::SHARED_WORDS + G * F::LDS_WORDS];
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
   const uint32_t item = blockIdx.x * G + team;
   const bool active = team < G && item < n;
-  uint32_t* my = lds + (team < G ? team : 0) * F::LDS_WORDS;
+  uint32_t* my = lds + F::SHARED_WORDS + (team < G ? team : 0) * F::LDS_WORDS;
   const uint32_t R = f.rounds();
   for (uint32_t r = 0; r < R; ++r) {
-    if (active) f(item, lane, r, my);
+    if (active) f(item, lane, r, my, lds);
     __syncthreads();
   }
 }

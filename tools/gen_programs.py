@@ -967,7 +967,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--team", type=int, default=32)
     ap.add_argument("--fexp-team", type=int, default=16)
-    ap.add_argument("--g2-team", type=int, default=8)
+    ap.add_argument("--g2-team", type=int, default=16)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--out", default=os.path.join(ROOT, "light-client-consensus-specs_amd", "csrc", "lcv_programs.inc"))
     args = ap.parse_args()
