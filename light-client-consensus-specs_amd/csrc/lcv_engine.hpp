@@ -66,8 +66,8 @@ LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds
     uint32_t br = 0;
     LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(PL[j], v[j], br, br);  // d = p - v in [1, p]
     const uint32_t a = (uint32_t)(c < 0 ? -c : c);
-    const uint32_t negm = c < 0 ? 0xFFFFFFFFu : 0u;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = (d[j] & negm) | (v[j] & ~negm);
+    const bool neg = c < 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = neg ? d[j] : v[j];  // v_cndmask
     if (maxc <= 2) {
       for (uint32_t rep = 0; rep < maxc; ++rep) {
         const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;

@@ -107,6 +107,56 @@ LCV_FN void fp_mul_impl(uint32_t r[12], const uint32_t a[12], const uint32_t b[1
   fp_reduce_once(r, t);
 }
 
+// Device: product-scanning (FIPS) Montgomery multiplication on a 96-bit column accumulator.  One
+// multiply-accumulate = v_mad_u64_u32 (64-bit addend, carry-out to an SGPR pair) + v_addc_co_u32
+// into the top word: 2 instructions per 32x32 product instead of CIOS's mad + carry fix-ups.
+// Operands may be <= 2p (the engine's lazily reduced combinations): ab + mp < 2^384 * 3p.
+#ifndef LCV_FP_PS
+#define LCV_FP_PS 1
+#endif
+#if LCV_FP_PS && !defined(LCV_HOSTSIM)
+LCV_FN void mac_vv(uint64_t& acc, uint32_t& hi, uint32_t x, uint32_t y) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1"
+      : "+v"(acc), "=&s"(cc), "+v"(hi)
+      : "v"(x), "v"(y));
+}
+LCV_FN void mac_vs(uint64_t& acc, uint32_t& hi, uint32_t x, uint32_t y) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, %2, 0, %1"
+      : "+v"(acc), "=&s"(cc), "+v"(hi)
+      : "v"(x), "s"(y));
+}
+LCV_FN void fp_mul_ps(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint32_t m[12], t[12];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) {
+    LCV_UNROLL for (int i = 0; i < k; ++i) mac_vs(acc, hi, m[i], PL[k - i]);
+    LCV_UNROLL for (int i = 0; i <= k; ++i) mac_vv(acc, hi, a[i], b[k - i]);
+    m[k] = (uint32_t)acc * LCV_NP0;
+    mac_vs(acc, hi, m[k], PL[0]);  // low word becomes 0
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  LCV_UNROLL for (int k = 12; k < 23; ++k) {
+    LCV_UNROLL for (int i = k - 11; i < 12; ++i) {
+      mac_vv(acc, hi, a[i], b[k - i]);
+      mac_vs(acc, hi, m[i], PL[k - i]);
+    }
+    t[k - 12] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[11] = (uint32_t)acc;
+  fp_reduce_once(r, t);
+}
+#define LCV_MUL_IMPL fp_mul_ps
+#else
+#define LCV_MUL_IMPL fp_mul_impl
+#endif
+
 #if LCV_FP_CALL && !defined(LCV_HOSTSIM)
 struct fp_ret { uint32_t v[12]; };
 // Limbs travel as 24 scalar VGPR arguments / 12 returned VGPRs (clang's AMDGPU ABI passes
@@ -119,7 +169,7 @@ __device__ __noinline__ fp_ret fp_mul_call(uint32_t a0, uint32_t a1, uint32_t a2
   const uint32_t a[12] = {a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11};
   const uint32_t b[12] = {b0, b1, b2, b3, b4, b5, b6, b7, b8, b9, b10, b11};
   fp_ret r;
-  fp_mul_impl(r.v, a, b);
+  LCV_MUL_IMPL(r.v, a, b);
   return r;
 }
 LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
@@ -131,7 +181,7 @@ LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
 #else
 LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
   LCV_COUNT(0);
-  fp_mul_impl(r.v, a.v, b.v);
+  LCV_MUL_IMPL(r.v, a.v, b.v);
 }
 #endif
 
