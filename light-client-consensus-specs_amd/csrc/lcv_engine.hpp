@@ -9,23 +9,27 @@
 // allocator guarantees it), so a barrier between rounds is the only synchronisation.  The Fp
 // arithmetic is the same 12 x 32-bit Montgomery code as everywhere else (lcv_field.hpp).
 //
-// Encoding (uint16): round header [nA, nB, stride, used], then `used` entries of `stride` words:
-//   dst | 0x1000 (MUL) | 0x2000 (INV),  nA terms,  nB terms;   term = slot | coef << 12 (4-bit signed)
-// (header words 0/1: n | max|coef| << 8 | reduction bits << 11 | full << 14; slots >= nslots are constants)
+// Encoding (tools/gen_programs.py Program.encode): per round two wave-uniform header words and, per
+// lane, a fixed 32-byte record (16 x uint16: dst | MUL << 12 | INV << 13, A terms from halfword 1,
+// B terms from halfword LCV_PROG_B_AT; term = slot | coef << 12, signed 4-bit, padding = slot 0 coef 0).
+// Fixed-size records let the kernel prefetch round r+1 (two 16-byte loads + the header) while it
+// executes round r, so no global-memory latency sits on the round's critical path.
 #pragma once
 #include "lcv_items.hpp"
+#include "lcv_programs.inc"
 
 namespace lcv {
 
 enum { ENG_SLOT_NONE = 0xFFF, ENG_MUL = 0x1000, ENG_INV = 0x2000 };
 
 struct ProgView {
-  const uint16_t* words;
-  const uint32_t* offs;
+  const uint32_t* hdr;     // 2 words per round
+  const uint32_t* rec;     // LCV_PROG_REC_HW / 2 words per lane per round, TEAM lanes per round
   const uint32_t* consts;  // 12 limbs per constant (Montgomery), copied into LDS slots nslots..
   uint32_t rounds;
   uint32_t nslots, nconst;
 };
+enum { ENG_REC_WORDS = LCV_PROG_REC_HW / 2 };
 
 // prologue helper: the program's constants go to the block's shared LDS region `cl` (slot nslots + k
 // is constant k); every team writes the same values, the round barrier publishes them
@@ -42,88 +46,109 @@ LCV_FN void eng_store(uint32_t* lds, uint32_t slot, const fp& v) {
   LCV_UNROLL for (int k = 0; k < 12; ++k) dst[k] = v.v[k];
 }
 
-// out = sum_k c_k * value(slot_k) (mod p).  Branch-free and uniform across the wave: the round
-// header h gives n (terms), maxc (largest |c| in the round), k (2^k > sum |c|) and whether the
-// result must be fully reduced (< p, LIN results are stored) or only <= 2p (a Montgomery operand:
-// a, b <= 2p gives ab < R p and a result < 2p).  Each term adds |c| * v (c > 0) or |c| * (p - v)
-// (c < 0, p - v in [1, p]) into an UNREDUCED 13-limb accumulator (< 2^k p <= 2^6 p), then
-// conditional subtraction of 2^s p for s = k-1 .. (full ? 0 : 1).  |c| * v: masked repeated
-// addition when maxc <= 2, else a v_mad_u64_u32 chain (cost independent of |c|).
-LCV_FN void eng_eval(fp& out, const uint16_t* t, uint32_t h, const uint32_t* lds, const uint32_t* cl, uint32_t ns) {
+// halfword j of a lane record (j is a compile-time constant after unrolling)
+LCV_FN uint32_t eng_hw(const uint32_t* w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; }
+
+LCV_FN const uint32_t* eng_src(uint32_t term, const uint32_t* lds, const uint32_t* cl, uint32_t ns) {
+  const uint32_t slot = term & 0xFFFu;
+  return slot >= ns ? cl + 12 * (slot - ns) : lds + 12 * slot;
+}
+
+// out = sum_k c_k * value(slot_k) (mod p) over the NMAX-unrolled terms at halfwords BASE.. of the
+// record; n, maxc, kb, lo are wave-uniform (round header), so every branch below is scalar.  Each term
+// adds |c| * v (c > 0) or |c| * (p - v) (c < 0, p - v in [1, p]) into an UNREDUCED 13-limb
+// accumulator (< 2^kb p <= 2^6 p), then conditional subtraction of 2^s p for s = kb-1 .. lo: lo = 0
+// fully reduces (LIN results are stored), lo = 1 leaves <= 2p (a Montgomery operand: a, b <= 2p gives
+// ab < R p and a result < 2p).  |c| * v: masked repeated addition when maxc <= 2, else a
+// v_mad_u64_u32 chain.  The LDS read of term k+1 is issued before term k is accumulated.
+template <int BASE, int NMAX>
+LCV_FN void eng_eval(fp& out, const uint32_t* w, uint32_t n, uint32_t maxc, uint32_t kb, uint32_t lo,
+                     const uint32_t* lds, const uint32_t* cl, uint32_t ns) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
-  const uint32_t n = h & 0xFFu, maxc = (h >> 8) & 7u, kb = (h >> 11) & 7u, lo = (h >> 14) & 1u ? 0u : 1u;
   uint32_t acc[13];
   LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = 0;
-  for (uint32_t k = 0; k < n; ++k) {
-    const uint32_t w = t[k];
-    uint32_t slot = w & 0xFFFu;
-    int c = (int)(w >> 12);
-    if (c >= 8) c -= 16;
-    if (slot == ENG_SLOT_NONE) { slot = 0; c = 0; }
-    const uint32_t* src = slot >= ns ? cl + 12 * (slot - ns) : lds + 12 * slot;
-    uint32_t v[12], d[12];
+  uint32_t v[12];
+  {
+    const uint32_t* src = eng_src(eng_hw(w, BASE), lds, cl, ns);
     LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = src[j];
-    uint32_t br = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(PL[j], v[j], br, br);  // d = p - v in [1, p]
+  }
+  LCV_UNROLL for (int k = 0; k < NMAX; ++k) {
+    if ((uint32_t)k >= n) break;
+    const uint32_t term = eng_hw(w, BASE + k);
+    uint32_t nx[12];
+    if (k + 1 < NMAX && (uint32_t)(k + 1) < n) {
+      const uint32_t* src = eng_src(eng_hw(w, BASE + (k + 1 < NMAX ? k + 1 : k)), lds, cl, ns);
+      LCV_UNROLL for (int j = 0; j < 12; ++j) nx[j] = src[j];
+    }
+    int c = (int)(term >> 12);
+    if (c >= 8) c -= 16;
     const uint32_t a = (uint32_t)(c < 0 ? -c : c);
     const bool neg = c < 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = neg ? d[j] : v[j];  // v_cndmask
+    uint32_t d[12], br = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(PL[j], v[j], br, br);  // p - v in [1, p]
+    LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = neg ? d[j] : v[j];             // v_cndmask
     if (maxc <= 2) {
       for (uint32_t rep = 0; rep < maxc; ++rep) {
         const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;
         uint32_t cy = 0;
-        LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], v[j] & keep, cy, cy);
+        LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], d[j] & keep, cy, cy);
         acc[12] += cy;
       }
     } else {
       uint32_t hi = 0, cy = 0;
       LCV_UNROLL for (int j = 0; j < 12; ++j) {
-        const uint64_t pr = (uint64_t)v[j] * a + hi;  // < 2^35: one v_mad_u64_u32
+        const uint64_t pr = (uint64_t)d[j] * a + hi;  // < 2^35: one v_mad_u64_u32
         hi = (uint32_t)(pr >> 32);
         acc[j] = addc32(acc[j], (uint32_t)pr, cy, cy);
       }
       acc[12] += hi + cy;
     }
-  }
-  for (uint32_t s = kb; s-- > lo;) {  // acc < 2^kb p  ->  acc < 2^lo p
-    uint32_t sp[13], d[13];
-    uint32_t cy = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) {  // sp = p << s
-      sp[j] = (PL[j] << s) | cy;
-      cy = s ? (PL[j] >> (32 - s)) : 0u;
+    if (k + 1 < NMAX && (uint32_t)(k + 1) < n) {
+      LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = nx[j];
     }
-    sp[12] = cy;
-    uint32_t br = 0;
-    LCV_UNROLL for (int j = 0; j < 13; ++j) d[j] = subc32(acc[j], sp[j], br, br);
-    LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = br ? acc[j] : d[j];
+  }
+  // acc < 2^kb p  ->  acc < 2^lo p; s is a constant after unrolling, so p << s folds into literals
+  LCV_UNROLL for (int s = 5; s >= 0; --s) {
+    if ((uint32_t)s < kb && (uint32_t)s >= lo) {
+      uint32_t sp[13], dd[13];
+      LCV_UNROLL for (int j = 0; j < 12; ++j) sp[j] = (PL[j] << s) | (s && j ? (PL[j - 1] >> (32 - s)) : 0u);
+      sp[12] = s ? (PL[11] >> (32 - s)) : 0u;
+      uint32_t br = 0;
+      LCV_UNROLL for (int j = 0; j < 13; ++j) dd[j] = subc32(acc[j], sp[j], br, br);
+      LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = br ? acc[j] : dd[j];
+    }
   }
   LCV_UNROLL for (int j = 0; j < 12; ++j) out.v[j] = acc[j];
 }
 
-// one round of a program for lane `lane` of the team whose LDS slots start at `lds`
-LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t* lds, const uint32_t* cl) {
-  const uint16_t* rp = P.words + P.offs[r];
-  const uint32_t hA = rp[0], hB = rp[1], stride = rp[2], used = rp[3];
-  const uint32_t nA = hA & 0xFFu;
-  if (lane >= used) return;
-  const uint16_t* e = rp + 4 + lane * stride;
-  const uint32_t dst = e[0];
+// one round for one lane: record w (ENG_REC_WORDS words), header h0/h1 (wave-uniform)
+LCV_FN void eng_exec(const uint32_t* w, uint32_t h0, uint32_t h1, uint32_t* lds, const uint32_t* cl, uint32_t ns) {
+  const uint32_t nA = h0 & 0xFu, mA = (h0 >> 4) & 0xFu, kA = (h0 >> 8) & 7u, loA = (h0 >> 11) & 1u ? 0u : 1u;
+  const uint32_t nB = (h0 >> 12) & 0xFu, mB = (h0 >> 16) & 0xFu, kB = (h0 >> 20) & 7u;
+  const uint32_t dst = eng_hw(w, 0);
   fp a;
-  eng_eval(a, e + 1, hA, lds, cl, P.nslots);
-  if (dst & ENG_MUL) {
-    fp b;
-    eng_eval(b, e + 1 + nA, hB, lds, cl, P.nslots);
-    fp_mul(a, a, b);
-  } else if (dst & ENG_INV) {
-    fp_inv_bingcd(a, a);
+  eng_eval<1, LCV_PROG_KLIN>(a, w, nA, mA, kA, loA, lds, cl, ns);
+  if (h1 & 0x100u) {  // a MUL round (B operands have <= 4 terms); LIN lanes keep A
+    fp b, m;
+    eng_eval<LCV_PROG_B_AT, LCV_PROG_REC_HW - LCV_PROG_B_AT>(b, w, nB, mB, kB, 1u, lds, cl, ns);
+    fp_mul(m, a, b);
+    if (dst & ENG_MUL) a = m;
   }
-  eng_store(lds, dst & 0xFFFu, a);
+  if (h1 & 0x200u) {
+    if (dst & ENG_INV) fp_inv_bingcd(a, a);
+  }
+  if ((dst & 0xFFFu) != ENG_SLOT_NONE) eng_store(lds, dst & 0xFFFu, a);
+}
+
+// one round of a program for lane `lane` (host simulation and the generic round loop)
+LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t team, uint32_t* lds, const uint32_t* cl) {
+  const uint32_t* w = P.rec + ((size_t)r * team + lane) * ENG_REC_WORDS;
+  eng_exec(w, P.hdr[2 * r], P.hdr[2 * r + 1], lds, cl, P.nslots);
 }
 
 }  // namespace lcv
 
 // ============================================================================ pairing stages
-#include "lcv_programs.inc"
 
 namespace lcv {
 
@@ -168,7 +193,7 @@ LCV_FN void item_miller_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* ld
     eng_load_consts(P, lane, LCV_PROG_MILLER_TEAM, cl);
     miller_prologue(i, lane, lds, W);
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds, cl);
+    eng_round(P, r - 1, lane, LCV_PROG_MILLER_TEAM, lds, cl);
   } else if (lane < 12) {
     fp v;
     eng_load(v, lds, LCV_PROG_MILLER_SLOT_F0_0 + lane);
@@ -185,7 +210,7 @@ LCV_FN void item_fexp_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds,
     soa_ld_fp(v, W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u));
     eng_store(lds, LCV_PROG_FEXP_SLOT_F0_0 + lane, v);
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds, cl);
+    eng_round(P, r - 1, lane, LCV_PROG_FEXP_TEAM, lds, cl);
   } else if (lane < 12) {
     fp v;
     eng_load(v, lds, LCV_PROG_FEXP_SLOT_R0_0 + lane);
@@ -214,7 +239,7 @@ LCV_FN void item_h2c_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, 
       eng_store(lds, LCV_PROG_H2C_SLOT_M0X0 + k, v);
     }
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds, cl);
+    eng_round(P, r - 1, lane, LCV_PROG_H2C_TEAM, lds, cl);
   } else if (lane < 4) {
     fp v;
     eng_load(v, lds, LCV_PROG_H2C_SLOT_HX0 + lane);
@@ -238,7 +263,7 @@ LCV_FN void item_g2sub_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds
       eng_store(lds, LCV_PROG_G2SUB_SLOT_SX0 + k, v);
     }
   } else if (r <= P.rounds) {
-    eng_round(P, r - 1, lane, lds, cl);
+    eng_round(P, r - 1, lane, LCV_PROG_G2SUB_TEAM, lds, cl);
   } else if (lane == 0 && W.sig_status[i] == PT_OK) {
     bool e_zero = true;
     for (uint32_t k = 0; k < 4; ++k) {

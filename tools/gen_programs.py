@@ -36,7 +36,9 @@ P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB1
 X_ABS = 0xD201000000010000
 RM = 1 << 384
 KOP = 4            # max terms of a MUL operand combination (longer ones are materialised by LIN ops)
-KLIN = 12          # max terms of one LIN op
+KLIN = 11          # max terms of one LIN op (record halfwords 1..11)
+REC_HW = 16        # uint16 per lane record: dst, A terms from 1, B terms from B_AT
+B_AT = 12          # MUL operand B at rec[12..15] (KOP <= 4)
 COEF_MAX = 7       # term coefficients are signed 4-bit
 SLOT_NONE = 0xFFF
 CONST_BASE = 3072  # slots >= CONST_BASE index the constant table
@@ -737,12 +739,18 @@ class Program:
 
     # ---------------------------------------------------------------- encoding
     def encode(self):
-        """uint16 words.  Round r at offs[r]: [hA, hB, stride, used], h = n | maxc << 8 | k << 11 |
-        full << 14 (n terms, max |coef|, reduction bits k, full reduction), then `used`
-        lane entries of `stride` words: dst | flags, nA terms, nB terms.  dst bits 0-11 slot, bit 12
-        MUL, bit 13 INV.  term = slot (bits 0-11) | coef (bits 12-15, two's complement, 0 = padding).
+        """Fixed-size records, so the device can prefetch round r+1 while it executes round r.
+
+        hdr: two uint32 per round (wave-uniform):
+          hdr[2r]   = nA | mA << 4 | kA << 8 | fullA << 11 | nB << 12 | mB << 16 | kB << 20
+          hdr[2r+1] = used | any_mul << 8 | any_inv << 9
+        (n terms, max |coef|, reduction bits k with 2^k > sum |coef|, full reduction of A).
+        rec: REC_HW uint16 per lane per round, T lanes per round (lanes >= used: dst = SLOT_NONE):
+          rec[0] = dst | MUL << 12 | INV << 13;  A terms at rec[1 .. 1+nA);  B terms at rec[B_AT ..]
+          term = slot | coef << 12 (signed 4-bit); padding = slot 0, coef 0 (adds nothing).
         Slots >= nslots are the constant table (copied into LDS by the kernel prologue)."""
-        words, offs = [], []
+        hdr, rec = [], []
+        T = self.team
         for cur in self.rounds:
             ents = []
             for v in cur:
@@ -756,54 +764,65 @@ class Program:
             # reduction of the unreduced accumulator (< S p, S = sum |c|): conditional subtraction of
             # 2^s p for s = k-1 .. lo with 2^k > S; lo = 0 (< p: LIN results are stored) or 1
             # (<= 2p suffices for a Montgomery operand: a, b <= 2p -> ab < R p)
-            def kbits(S):
-                return S.bit_length()  # smallest k with 2^k > S
-            kA = max(kbits(sum(abs(c) for _, c in a)) for _, a, _ in ents)
+            kA = max(sum(abs(c) for _, c in a).bit_length() for _, a, _ in ents)
             fullA = any(v.kind != "mul" for v, _, _ in ents)
-            kB = max((kbits(sum(abs(c) for _, c in b)) for v, _, b in ents if v.kind == "mul"), default=0)
-            assert kA <= 6 and kB <= 6 and mA <= 7 and mB <= 7
-            stride = 1 + nA + nB
-            offs.append(len(words))
-            words += [nA | (mA << 8) | (kA << 11) | ((1 if fullA else 0) << 14),
-                      nB | (mB << 8) | (kB << 11), stride, len(ents)]
-            for v, a, b in ents:
-                flags = (1 << 12) if v.kind == "mul" else (1 << 13) if v.kind == "inv" else 0
-                words.append(v.slot | flags)
-                for terms, n in ((a, nA), (b, nB)):
-                    for u, c in terms:
+            anymul = any(v.kind == "mul" for v, _, _ in ents)
+            anyinv = any(v.kind == "inv" for v, _, _ in ents)
+            kB = max((sum(abs(c) for _, c in b).bit_length() for v, _, b in ents if v.kind == "mul"), default=0)
+            assert kA <= 6 and kB <= 6 and mA <= 7 and mB <= 7 and nA <= B_AT - 1 and nB <= REC_HW - B_AT
+            assert not anymul or nA <= B_AT - 1
+            hdr += [nA | (mA << 4) | (kA << 8) | ((1 if fullA else 0) << 11) | (nB << 12) | (mB << 16) | (kB << 20),
+                    len(ents) | ((1 if anymul else 0) << 8) | ((1 if anyinv else 0) << 9)]
+            for lane in range(T):
+                w = [0] * REC_HW
+                if lane < len(ents):
+                    v, a, b = ents[lane]
+                    flags = (1 << 12) if v.kind == "mul" else (1 << 13) if v.kind == "inv" else 0
+                    w[0] = v.slot | flags
+                    for k, (u, c) in enumerate(a):
                         assert -8 <= c <= 7 and c != 0, c
-                        words.append(u.slot | ((c & 0xF) << 12))
-                    words += [SLOT_NONE] * (n - len(terms))
-        return words, offs
+                        w[1 + k] = u.slot | ((c & 0xF) << 12)
+                    for k, (u, c) in enumerate(b):
+                        assert -8 <= c <= 7 and c != 0, c
+                        w[B_AT + k] = u.slot | ((c & 0xF) << 12)
+                else:
+                    w[0] = SLOT_NONE
+                rec += w
+        return hdr, rec
 
     # ---------------------------------------------------------------- emulation (round semantics)
     def emulate(self, inputs):
+        """Execute the ENCODED program with Python integers (the device's round semantics)."""
         mem = {}
         for name, v in self.tr.inputs.items():
             mem[v.slot] = inputs[name] % P
         consts = {self.nslots + k: c for k, c in enumerate(self.consts)}
-        words, offs = self.encode()
-        for r, off in enumerate(offs):
-            nA, nB, stride, used = words[off:off + 4]
-            nA, nB = nA & 0xFF, nB & 0xFF  # (bits 8+: coefficient / reduction metadata)
+        hdr, rec = self.encode()
+        T = self.team
+        for r in range(len(hdr) // 2):
+            h0, h1 = hdr[2 * r], hdr[2 * r + 1]
+            nA, nB, used = h0 & 0xF, (h0 >> 12) & 0xF, h1 & 0xFF
             writes = []
-            for lane in range(used):
-                e = words[off + 4 + lane * stride: off + 4 + (lane + 1) * stride]
+            for lane in range(T):
+                e = rec[(r * T + lane) * REC_HW:(r * T + lane + 1) * REC_HW]
                 dst = e[0]
+                if lane >= used:
+                    assert dst == SLOT_NONE
+                    continue
 
                 def ev(ts):
                     acc = 0
                     for t in ts:
                         s, c = t & 0xFFF, (t >> 12) & 0xF
-                        if s == SLOT_NONE or c == 0:
-                            continue
                         c = c - 16 if c >= 8 else c
+                        if c == 0:
+                            continue
                         val = consts[s] if s >= self.nslots else mem[s]
                         acc = (acc + c * val) % P
                     return acc
                 A = ev(e[1:1 + nA])
                 if dst & (1 << 12):
-                    res = A * ev(e[1 + nA:1 + nA + nB]) % P
+                    res = A * ev(e[B_AT:B_AT + nB]) % P
                 elif dst & (1 << 13):
                     res = pow(A, P - 2, P)
                 else:
@@ -933,25 +952,26 @@ def check_g2sub(prog):
 
 def emit(progs, path):
     lines = ["// GENERATED by tools/gen_programs.py — do not edit.  Team programs (see lcv_engine.hpp).",
-             "#pragma once", "#include <stdint.h>", ""]
+             "#pragma once", "#include <stdint.h>", "",
+             f"#define LCV_PROG_REC_HW {REC_HW}", f"#define LCV_PROG_B_AT {B_AT}", f"#define LCV_PROG_KLIN {KLIN}", ""]
     for p in progs:
-        words, offs = p.encode()
+        hdr, rec = p.encode()
         N = p.name.upper()
         lines.append(f"// {p.stats()}")
         lines.append(f"#define LCV_PROG_{N}_TEAM {p.team}")
-        lines.append(f"#define LCV_PROG_{N}_ROUNDS {len(offs)}")
+        lines.append(f"#define LCV_PROG_{N}_ROUNDS {len(hdr) // 2}")
         lines.append(f"#define LCV_PROG_{N}_SLOTS {p.nslots}")
         lines.append(f"#define LCV_PROG_{N}_NCONST {len(p.consts)}")
         lines.append(f"#define LCV_PROG_{N}_MAXSUM {p.max_abs_sum()}")
         for nm, s in sorted(p.state_slots.items(), key=lambda kv: kv[1]):
             lines.append(f"#define LCV_PROG_{N}_SLOT_{nm.upper()} {s}")
-        lines.append(f"static const uint16_t kProg_{p.name}_words[{len(words)}] = {{")
-        for i in range(0, len(words), 24):
-            lines.append("  " + ",".join(str(w) for w in words[i:i + 24]) + ",")
+        lines.append(f"static const uint32_t kProg_{p.name}_hdr[{len(hdr)}] = {{")
+        for i in range(0, len(hdr), 16):
+            lines.append("  " + ",".join(str(w) for w in hdr[i:i + 16]) + ",")
         lines.append("};")
-        lines.append(f"static const uint32_t kProg_{p.name}_offs[{len(offs)}] = {{")
-        for i in range(0, len(offs), 16):
-            lines.append("  " + ",".join(str(o) for o in offs[i:i + 16]) + ",")
+        lines.append(f"static const uint16_t kProg_{p.name}_rec[{len(rec)}] __attribute__((aligned(16))) = {{")
+        for i in range(0, len(rec), 32):
+            lines.append("  " + ",".join(str(w) for w in rec[i:i + 32]) + ",")
         lines.append("};")
         # constants: Montgomery form, 12 little-endian 32-bit limbs each
         lines.append(f"static const uint32_t kProg_{p.name}_consts[{max(1, len(p.consts)) * 12}] = {{")
