@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--participation", default="full", choices=["full", "random"])
     ap.add_argument("--cpu-sample", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", default="1,1", help="STREAMS,SLICES of the timed run (1,1 = serial stages)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,6 +86,8 @@ def main():
     log(f"[rank {rank}] generated {args.n} updates in {time.perf_counter() - t0:.1f}s")
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     rb = v.upload(sb.updates)
+    pipe = tuple(int(x) for x in args.pipeline.split(","))
+    v.set_pipeline(*pipe)
     verdict = np.zeros(args.n, np.uint8)
     reason = np.zeros(args.n, np.uint8)
 
@@ -117,14 +120,10 @@ def main():
         import torch
         torch.cuda.synchronize()
         ok_all = bool((gathered == 1).all().item())
-    stage_ms = {k: 0.0 for k in v.last_timings()}
-
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for k, ms in v.last_timings().items():
-            stage_ms[k] += ms
     sync()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -132,6 +131,20 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+
+    # per-stage kernel times (HIP events on each stage's stream) come from the serial shape, where
+    # no other kernel shares the GPU: the roofline of the dominant kernel is measured there, outside
+    # the timed region above; the serial step time is reported beside `value`
+    v.set_pipeline(1, 1)
+    stage_ms = {k: 0.0 for k in v.last_timings()}
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
+        for k, ms in v.last_timings().items():
+            stage_ms[k] += ms
+    serial_ms = 1000 * (time.perf_counter() - ts) / args.steps
+    serial_ok = bool((verdict == 1).all())
+    v.set_pipeline(*pipe)
 
     # PCIe-inclusive rate (host batch -> device each time), reported beside `value`, never as it
     t1 = time.perf_counter()
@@ -147,6 +160,10 @@ def main():
     stage_avg = {k: round(ms / args.steps, 3) for k, ms in stage_ms.items()}
     kernel_ms = sum(stage_avg.values())
     roof = roofline(stage_avg, args.n)
+    if roof is not None:  # the whole pipeline's rate against the same peak (all stages, all kernels)
+        roof["pipeline_ops_per_update"] = total_ops_per_update()
+        roof["pipeline_achieved"] = round(roof["pipeline_ops_per_update"] * total / dt / world / 1e12, 3)
+        roof["pipeline_frac"] = round(roof["pipeline_achieved"] / PEAK_INT32_TOPS, 4)
     out = {
         "metric": "verified LightClientUpdates/sec (512-member committee)",
         "value": round(total / dt, 1),
@@ -163,9 +180,11 @@ def main():
         "config": {"workload": f"configs[1]: {args.n} updates/GPU, {args.participation} participation, "
                                f"next_sync_committee + finality + execution branches",
                    "updates_per_gpu": args.n, "committee": 512, "parallelism": f"dp{world} (independent updates)"},
-        "all_valid": ok_all,
-        "kernel_ms_per_step": round(kernel_ms, 3),
-        "stage_ms_per_step": stage_avg,
+        "all_valid": ok_all and serial_ok,
+        "pipeline": {"streams": pipe[0], "slices": pipe[1]},
+        "serial_ms_per_step": round(serial_ms, 3),
+        "serial_kernel_ms_per_step": round(kernel_ms, 3),
+        "serial_stage_ms_per_step": stage_avg,
         "pcie_inclusive_updates_per_s_1gpu": round(pcie_rate, 1),
         "roofline": roof,
     }
@@ -178,6 +197,11 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def total_ops_per_update():
+    c = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["total_per_update"]
+    return 600 * c["fp_mul"] + 24 * c["fp_add"] + 2100 * c["sha"]
 
 
 def roofline(stage_ms: dict, n: int):

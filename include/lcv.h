@@ -110,7 +110,13 @@ int lcv_validate_resident(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot, co
 /* same, verdicts written to a DEVICE buffer of n bytes (for an RCCL all-gather); no host copy */
 int lcv_validate_resident_dev(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot,
                               const uint8_t* genesis_validators_root, uint8_t* verdict_dev);
-/* kernel time of the last validate call: total and per stage (ms); names via lcv_stage_name */
+/* Execution shape of lcv_validate_*: each 64k-update chunk is cut into `chunks` slices whose whole
+ * stage chains run on min(streams, 4) HIP streams, so different slices' kernels overlap.  streams = 1
+ * (default) runs the stages one after another over the whole chunk (per-stage timings available);
+ * verdicts are identical either way.  Performance knob only, no reference counterpart. */
+int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
+/* kernel time of the last validate call: total and per stage (ms); names via lcv_stage_name
+ * (stage times are recorded by the serial shape only: zero under a multi-stream pipeline) */
 int lcv_last_timings(lcv_ctx* ctx, float* ms_out, int max_stages, int* nstages);
 const char* lcv_stage_name(int stage);
 

@@ -13,18 +13,18 @@
 
 struct lcv_ctx;
 
+enum { BE_STREAMS = 4 };  // GPU_MAX_HW_QUEUES on the box: one hardware queue per stream
 struct Backend {
-  hipStream_t stream = nullptr;   // main stream: copies + the current launch stream when cur == 0
-  hipStream_t side = nullptr;     // second stream for independent stages (be_fork / be_join)
-  int cur = 0;
+  hipStream_t st[BE_STREAMS] = {};  // st[0]: main stream (copies, serial stages); st[k]: forked work
+  int cur = 0;                      // stream of the next launch / copy
   int device = 0;
   struct Mark { int stage; hipEvent_t a, b; };
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   std::vector<Mark> marks;
-  int open_stage[2] = {-1, -1};
-  hipEvent_t open_ev[2] = {nullptr, nullptr};
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  int open_stage[BE_STREAMS] = {-1, -1, -1, -1};
+  hipEvent_t open_ev[BE_STREAMS] = {};
+  hipEvent_t fork_ev[BE_STREAMS] = {}, join_ev[BE_STREAMS] = {};
 };
 
 static int be_init(lcv_ctx* ctx, int device);
@@ -36,6 +36,9 @@ static int be_d2h(lcv_ctx* ctx, void* dst, const void* src, size_t bytes);
 static int be_d2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes);
 static int be_memset(lcv_ctx* ctx, void* p, int v, size_t bytes);
 static int be_sync(lcv_ctx* ctx);
+static int be_fork_to(lcv_ctx* ctx, int k);
+static int be_join_from(lcv_ctx* ctx, int k);
+static int be_nstreams() { return BE_STREAMS; }
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
 static int be_fork(lcv_ctx* ctx);
@@ -58,26 +61,30 @@ static int hip_fail(lcv_ctx* ctx, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(ctx, _e, #x); \
   } while (0)
 
+static hipStream_t cur_stream(lcv_ctx* ctx) { return ctx->be.st[ctx->be.cur]; }
+
 static int be_init(lcv_ctx* ctx, int device) {
   int nd = 0;
   HIPCHK(ctx, hipGetDeviceCount(&nd));
   if (device < 0 || device >= nd) return fail(ctx, LCV_EDEVICE, "lcv_init: no such HIP device");
   ctx->be.device = device;
   HIPCHK(ctx, hipSetDevice(device));
-  HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->be.stream, hipStreamNonBlocking));
-  HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->be.side, hipStreamNonBlocking));
-  HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.fork_ev, hipEventDisableTiming));
-  HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.join_ev, hipEventDisableTiming));
+  for (int k = 0; k < BE_STREAMS; ++k) {
+    HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->be.st[k], hipStreamNonBlocking));
+    HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.fork_ev[k], hipEventDisableTiming));
+    HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.join_ev[k], hipEventDisableTiming));
+  }
   return LCV_OK;
 }
 
 static void be_destroy(lcv_ctx* ctx) {
   (void)hipSetDevice(ctx->be.device);
   for (hipEvent_t e : ctx->be.pool) (void)hipEventDestroy(e);
-  if (ctx->be.stream) (void)hipStreamDestroy(ctx->be.stream);
-  if (ctx->be.side) (void)hipStreamDestroy(ctx->be.side);
-  if (ctx->be.fork_ev) (void)hipEventDestroy(ctx->be.fork_ev);
-  if (ctx->be.join_ev) (void)hipEventDestroy(ctx->be.join_ev);
+  for (int k = 0; k < BE_STREAMS; ++k) {
+    if (ctx->be.st[k]) (void)hipStreamDestroy(ctx->be.st[k]);
+    if (ctx->be.fork_ev[k]) (void)hipEventDestroy(ctx->be.fork_ev[k]);
+    if (ctx->be.join_ev[k]) (void)hipEventDestroy(ctx->be.join_ev[k]);
+  }
 }
 
 static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
@@ -92,49 +99,48 @@ static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
 static void be_free(lcv_ctx* ctx, void* p) {
   if (!p) return;
   (void)hipSetDevice(ctx->be.device);
-  (void)hipStreamSynchronize(ctx->be.stream);
-  (void)hipStreamSynchronize(ctx->be.side);
+  for (int k = 0; k < BE_STREAMS; ++k) (void)hipStreamSynchronize(ctx->be.st[k]);
   (void)hipFree(p);
 }
 static int be_h2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (!bytes) return LCV_OK;
-  HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->be.stream));
+  HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cur_stream(ctx)));
   return LCV_OK;
 }
 static int be_d2h(lcv_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (!bytes) return LCV_OK;
-  HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->be.stream));
+  HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, cur_stream(ctx)));
   return LCV_OK;
 }
 static int be_d2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (!bytes) return LCV_OK;
-  HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->be.stream));
+  HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, cur_stream(ctx)));
   return LCV_OK;
 }
 static int be_memset(lcv_ctx* ctx, void* p, int v, size_t bytes) {
   if (!bytes) return LCV_OK;
-  HIPCHK(ctx, hipMemsetAsync(p, v, bytes, ctx->be.stream));
+  HIPCHK(ctx, hipMemsetAsync(p, v, bytes, cur_stream(ctx)));
   return LCV_OK;
 }
 static int be_sync(lcv_ctx* ctx) {
-  HIPCHK(ctx, hipStreamSynchronize(ctx->be.side));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->be.stream));
+  for (int k = BE_STREAMS - 1; k >= 0; --k) HIPCHK(ctx, hipStreamSynchronize(ctx->be.st[k]));
   return LCV_OK;
 }
-static hipStream_t cur_stream(lcv_ctx* ctx) { return ctx->be.cur ? ctx->be.side : ctx->be.stream; }
-static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = k ? 1 : 0; }
-// side stream starts after everything queued so far on the main stream
-static int be_fork(lcv_ctx* ctx) {
-  HIPCHK(ctx, hipEventRecord(ctx->be.fork_ev, ctx->be.stream));
-  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.side, ctx->be.fork_ev, 0));
+static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = (k > 0 && k < BE_STREAMS) ? k : 0; }
+// stream k starts after everything queued so far on the main stream
+static int be_fork_to(lcv_ctx* ctx, int k) {
+  HIPCHK(ctx, hipEventRecord(ctx->be.fork_ev[k], ctx->be.st[0]));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[k], ctx->be.fork_ev[k], 0));
   return LCV_OK;
 }
-// main stream continues after everything queued so far on the side stream
-static int be_join(lcv_ctx* ctx) {
-  HIPCHK(ctx, hipEventRecord(ctx->be.join_ev, ctx->be.side));
-  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.stream, ctx->be.join_ev, 0));
+// the main stream continues after everything queued so far on stream k
+static int be_join_from(lcv_ctx* ctx, int k) {
+  HIPCHK(ctx, hipEventRecord(ctx->be.join_ev[k], ctx->be.st[k]));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[0], ctx->be.join_ev[k], 0));
   return LCV_OK;
 }
+static int be_fork(lcv_ctx* ctx) { return be_fork_to(ctx, 1); }
+static int be_join(lcv_ctx* ctx) { return be_join_from(ctx, 1); }
 
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n) {
   if (n == 0) return LCV_OK;
@@ -180,7 +186,7 @@ static void be_stage_end(lcv_ctx* ctx, int stage) {
 static void be_reset_timings(lcv_ctx* ctx) {
   ctx->be.marks.clear();
   ctx->be.used = 0;
-  ctx->be.open_stage[0] = ctx->be.open_stage[1] = -1;
+  for (int k = 0; k < BE_STREAMS; ++k) ctx->be.open_stage[k] = -1;
   for (int s = 0; s < ST_COUNT; ++s) ctx->stage_ms[s] = 0.f;
 }
 static void be_collect_timings(lcv_ctx* ctx) {

@@ -39,6 +39,9 @@ template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t 
 static int be_fork(lcv_ctx*) { return 0; }
 static int be_join(lcv_ctx*) { return 0; }
 static void be_use_stream(lcv_ctx*, int) {}
+static int be_fork_to(lcv_ctx*, int) { return 0; }
+static int be_join_from(lcv_ctx*, int) { return 0; }
+static int be_nstreams() { return 4; }
 static void be_stage_begin(lcv_ctx* ctx, int stage);
 static void be_stage_end(lcv_ctx* ctx, int stage);
 static void be_reset_timings(lcv_ctx* ctx);

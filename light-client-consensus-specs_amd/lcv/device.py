@@ -128,6 +128,11 @@ class Verifier:
         except Exception:
             pass
 
+    def set_pipeline(self, streams: int, chunks: int) -> None:
+        """Run validate's per-update stage chain on `chunks` slices over `streams` HIP streams
+        (overlapping stages of different slices); (1, 1) = serial stages with per-stage timings."""
+        self._check(self.lib.lcv_set_pipeline(self.ctx, int(streams), int(chunks)), "lcv_set_pipeline")
+
     def last_timings(self) -> Dict[str, float]:
         ms = (C.c_float * 16)()
         n = C.c_int()

@@ -101,3 +101,11 @@ def test_validate_large_batch_properties(gpu_verifier):
     rb = gpu_verifier.upload(sb.updates)
     v2, r2 = gpu_verifier.validate_resident(rb, sb.current_slot, sb.genesis_validators_root)
     assert np.array_equal(r2, reason) and np.array_equal(v2.astype(bool), ok)
+    # every execution shape (serial stages; slices over 2..4 streams, ragged last slice) agrees
+    try:
+        for shape in [(1, 1), (2, 3), (4, 7), (4, 32)]:
+            gpu_verifier.set_pipeline(*shape)
+            v3, r3 = gpu_verifier.validate_resident(rb, sb.current_slot, sb.genesis_validators_root)
+            assert np.array_equal(r3, reason), shape
+    finally:
+        gpu_verifier.set_pipeline(1, 1)
