@@ -55,18 +55,23 @@ LCV_FN const uint32_t* eng_src(uint32_t term, const uint32_t* lds, const uint32_
 }
 
 // out = sum_k c_k * value(slot_k) (mod p) over the NMAX-unrolled terms at halfwords BASE.. of the
-// record; n, maxc, kb, lo are wave-uniform (round header), so every branch below is scalar.  Each term
-// adds |c| * v (c > 0) or |c| * (p - v) (c < 0, p - v in [1, p]) into an UNREDUCED 13-limb
-// accumulator (< 2^kb p <= 2^6 p), then conditional subtraction of 2^s p for s = kb-1 .. lo: lo = 0
-// fully reduces (LIN results are stored), lo = 1 leaves <= 2p (a Montgomery operand: a, b <= 2p gives
-// ab < R p and a result < 2p).  |c| * v: masked repeated addition when maxc <= 2, else a
-// v_mad_u64_u32 chain.  The LDS read of term k+1 is issued before term k is accumulated.
+// record; n, maxc, kb, lo are wave-uniform (round header), so every branch below is scalar.  The
+// 13-limb accumulator starts at the bias 2^kb p (the signed sum lies in (-2^kb p, 2^kb p), 2^kb >
+// sum |c|) and each term adds t = |c| * v (< 7p < 2^384, 12 limbs) or its two's complement
+// (t ^ m) + 1 (m = all-ones when c < 0), so it stays in [0, 2^(kb+1) p) without any p - v.  Then
+// conditional subtraction of 2^s p for s = kb .. lo: lo = 0 fully reduces (LIN results are
+// stored), lo = 1 leaves < 2p (a Montgomery operand: a, b < 2p gives ab < R p, a result < 2p).
+// |c| * v: v itself when maxc = 1 (records pad with a zero constant at coefficient +1, so no
+// masking), a per-lane select of v / 2v when maxc = 2, else a v_mad_u64_u32 chain.  The LDS read of
+// term k+1 is issued before term k is accumulated.
 template <int BASE, int NMAX>
 LCV_FN void eng_eval(fp& out, const uint32_t* w, uint32_t n, uint32_t maxc, uint32_t kb, uint32_t lo,
                      const uint32_t* lds, const uint32_t* cl, uint32_t ns) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
   uint32_t acc[13];
-  LCV_UNROLL for (int j = 0; j < 13; ++j) acc[j] = 0;
+  acc[0] = PL[0] << kb;  // 1 <= kb <= 6 (wave-uniform: scalar shifts)
+  LCV_UNROLL for (int j = 1; j < 12; ++j) acc[j] = (PL[j] << kb) | (PL[j - 1] >> (32 - kb));
+  acc[12] = PL[11] >> (32 - kb);
   uint32_t v[12];
   {
     const uint32_t* src = eng_src(eng_hw(w, BASE), lds, cl, ns);
@@ -83,33 +88,32 @@ LCV_FN void eng_eval(fp& out, const uint32_t* w, uint32_t n, uint32_t maxc, uint
     int c = (int)(term >> 12);
     if (c >= 8) c -= 16;
     const uint32_t a = (uint32_t)(c < 0 ? -c : c);
-    const bool neg = c < 0;
-    uint32_t d[12], br = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = subc32(PL[j], v[j], br, br);  // p - v in [1, p]
-    LCV_UNROLL for (int j = 0; j < 12; ++j) d[j] = neg ? d[j] : v[j];             // v_cndmask
-    if (maxc <= 2) {
-      for (uint32_t rep = 0; rep < maxc; ++rep) {
-        const uint32_t keep = rep < a ? 0xFFFFFFFFu : 0u;
-        uint32_t cy = 0;
-        LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], d[j] & keep, cy, cy);
-        acc[12] += cy;
-      }
-    } else {
-      uint32_t hi = 0, cy = 0;
+    const uint32_t m = c < 0 ? 0xFFFFFFFFu : 0u;
+    uint32_t t[12];
+    if (maxc <= 1) {
+      LCV_UNROLL for (int j = 0; j < 12; ++j) t[j] = v[j];
+    } else if (maxc <= 2) {  // v < 2^381: 2v needs no 13th limb
+      const bool dbl = a == 2u;
+      t[0] = dbl ? v[0] << 1 : v[0];
+      LCV_UNROLL for (int j = 1; j < 12; ++j) t[j] = dbl ? ((v[j] << 1) | (v[j - 1] >> 31)) : v[j];
+    } else {  // |c| <= 7: |c| v < 2^384, the chain's last high word is 0
+      uint32_t hi = 0;
       LCV_UNROLL for (int j = 0; j < 12; ++j) {
-        const uint64_t pr = (uint64_t)d[j] * a + hi;  // < 2^35: one v_mad_u64_u32
+        const uint64_t pr = (uint64_t)v[j] * a + hi;  // one v_mad_u64_u32
+        t[j] = (uint32_t)pr;
         hi = (uint32_t)(pr >> 32);
-        acc[j] = addc32(acc[j], (uint32_t)pr, cy, cy);
       }
-      acc[12] += hi + cy;
     }
+    uint32_t cy = m & 1u;  // two's complement of t when c < 0: (t ^ m) + 1 over 13 limbs
+    LCV_UNROLL for (int j = 0; j < 12; ++j) acc[j] = addc32(acc[j], t[j] ^ m, cy, cy);
+    acc[12] = acc[12] + m + cy;
     if (k + 1 < NMAX && (uint32_t)(k + 1) < n) {
       LCV_UNROLL for (int j = 0; j < 12; ++j) v[j] = nx[j];
     }
   }
-  // acc < 2^kb p  ->  acc < 2^lo p; s is a constant after unrolling, so p << s folds into literals
-  LCV_UNROLL for (int s = 5; s >= 0; --s) {
-    if ((uint32_t)s < kb && (uint32_t)s >= lo) {
+  // acc < 2^(kb+1) p  ->  acc < 2^lo p; s is a constant after unrolling, so p << s folds into literals
+  LCV_UNROLL for (int s = 6; s >= 0; --s) {
+    if ((uint32_t)s <= kb && (uint32_t)s >= lo) {
       uint32_t sp[13], dd[13];
       LCV_UNROLL for (int j = 0; j < 12; ++j) sp[j] = (PL[j] << s) | (s && j ? (PL[j - 1] >> (32 - s)) : 0u);
       sp[12] = s ? (PL[11] >> (32 - s)) : 0u;

@@ -578,6 +578,9 @@ class Program:
         self.name, self.tr, self.team, self.policy, self.slack, self.cap = name, tr, team, policy, slack, cap
         self.outputs = outputs            # list of (name, F)
         self.state_slots = state_slots    # name -> slot for inputs/outputs sharing storage
+        if 0 not in tr.consts:            # the record padding term reads a zero constant
+            tr.consts[0] = tr._new("const", const=0)
+        self.zero = tr.consts[0]
         self.build()
 
     def build(self):
@@ -774,7 +777,9 @@ class Program:
             hdr += [nA | (mA << 4) | (kA << 8) | ((1 if fullA else 0) << 11) | (nB << 12) | (mB << 16) | (kB << 20),
                     len(ents) | ((1 if anymul else 0) << 8) | ((1 if anyinv else 0) << 9)]
             for lane in range(T):
-                w = [0] * REC_HW
+                # unused term positions: the zero constant at coefficient +1 (adds nothing, and the
+                # device's |c| = 1 path needs no mask)
+                w = [0] + [self.zero.slot | (1 << 12)] * (REC_HW - 1)
                 if lane < len(ents):
                     v, a, b = ents[lane]
                     flags = (1 << 12) if v.kind == "mul" else (1 << 13) if v.kind == "inv" else 0
