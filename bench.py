@@ -120,10 +120,15 @@ def main():
         import torch
         torch.cuda.synchronize()
         ok_all = bool((gathered == 1).all().item())
+    serial = pipe == (1, 1)
+    stage_ms = {k: 0.0 for k in v.last_timings()}
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+        if serial:  # stage kernel times: HIP events on each stage's stream, inside the timed region
+            for k, ms in v.last_timings().items():
+                stage_ms[k] += ms
     sync()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -132,19 +137,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # per-stage kernel times (HIP events on each stage's stream) come from the serial shape, where
-    # no other kernel shares the GPU: the roofline of the dominant kernel is measured there, outside
-    # the timed region above; the serial step time is reported beside `value`
-    v.set_pipeline(1, 1)
-    stage_ms = {k: 0.0 for k in v.last_timings()}
-    ts = time.perf_counter()
-    for _ in range(args.steps):
-        v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
-        for k, ms in v.last_timings().items():
-            stage_ms[k] += ms
-    serial_ms = 1000 * (time.perf_counter() - ts) / args.steps
-    serial_ok = bool((verdict == 1).all())
-    v.set_pipeline(*pipe)
+    serial_ms, serial_ok = 1000 * dt / args.steps, ok_all
+    if not serial:
+        # a multi-stream pipeline overlaps stages, so per-stage kernel times come from the serial
+        # shape (no other kernel sharing the GPU), run after the timed region
+        v.set_pipeline(1, 1)
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
+            for k, ms in v.last_timings().items():
+                stage_ms[k] += ms
+        serial_ms = 1000 * (time.perf_counter() - ts) / args.steps
+        serial_ok = bool((verdict == 1).all())
+        v.set_pipeline(*pipe)
 
     # PCIe-inclusive rate (host batch -> device each time), reported beside `value`, never as it
     t1 = time.perf_counter()
@@ -204,6 +209,30 @@ def total_ops_per_update():
     return 600 * c["fp_mul"] + 24 * c["fp_add"] + 2100 * c["sha"]
 
 
+# stages whose kernels merged into another stage's kernel (the Miller team program computes the lines
+# and the accumulation: its op count is the sum of both host-simulation stages)
+MERGED = {"miller_accumulate": ["miller_lines"], "sig_decode": ["miller_lines_sig"]}
+# the kernels of each stage (HBM traffic from profiles/traffic_pmc.json, tools/pmc_traffic.sh)
+STAGE_KERNELS = {"miller_accumulate": ["k_eng<F_eng_miller>"], "final_exp": ["k_eng<F_eng_fexp>"],
+                 "hash_to_g2": ["k_items<F_h2c_map>", "k_eng<F_eng_h2c>"],
+                 "sig_decode": ["k_items<F_sig>", "k_eng<F_eng_g2sub>"]}
+
+
+def stage_traffic(stage: str):
+    """HBM bytes per launch of a stage's kernels from the committed rocprofv3 PMC passes (FETCH_SIZE
+    doubled for gfx950 per MI355X_MICROARCH.md, + WRITE_SIZE), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic_pmc.json")
+    if not os.path.exists(path) or stage not in STAGE_KERNELS:
+        return None
+    t = json.load(open(path))
+    tot = 0.0
+    for k in STAGE_KERNELS[stage]:
+        if k not in t:
+            return None
+        tot += 2 * t[k]["FETCH_SIZE_KB_per_launch"] + t[k]["WRITE_SIZE_KB_per_launch"]
+    return round(tot * 1024)
+
+
 def roofline(stage_ms: dict, n: int):
     """Dominant kernel stage vs the INT32 VALU peak.  Algorithmic work per update per stage comes from
     profiles/opcounts.json (counted by the host-simulation build of the same kernels, tools/opcount.py):
@@ -213,14 +242,17 @@ def roofline(stage_ms: dict, n: int):
         return None
     counts = json.load(open(path))["per_update"]
     stage = max(stage_ms, key=lambda k: stage_ms[k])
-    c = counts.get(stage)
-    if c is None or stage_ms[stage] <= 0:
+    if stage not in counts or stage_ms[stage] <= 0:
         return None
-    ops = 600 * c["fp_mul"] + 24 * c["fp_add"] + 2100 * c["sha"]
+    ops = 0.0
+    for st in [stage] + MERGED.get(stage, []):
+        c = counts.get(st, {"fp_mul": 0, "fp_add": 0, "sha": 0})
+        ops += 600 * c["fp_mul"] + 24 * c["fp_add"] + 2100 * c["sha"]
     achieved = ops * n / (stage_ms[stage] * 1e-3) / 1e12
     return {"bound": "valu", "kernel": stage, "achieved": round(achieved, 3), "peak": PEAK_INT32_TOPS,
-            "unit": "T INT32 op/s", "frac": round(achieved / PEAK_INT32_TOPS, 4), "traffic": None,
-            "ops_per_update": ops}
+            "unit": "T INT32 op/s", "frac": round(achieved / PEAK_INT32_TOPS, 4),
+            "traffic": stage_traffic(stage), "traffic_unit": "B per launch (rocprofv3 PMC)",
+            "ops_per_update": ops, "ms_per_launch": stage_ms[stage]}
 
 
 if __name__ == "__main__":
