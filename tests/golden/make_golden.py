@@ -12,6 +12,11 @@ lc_updates.npz — light-client update cases (packed rows, include/lcv.h layouts
           names (oracle/spec.py: SSZ, compute_*, bls = oracle FastAggregateVerify);
       (2) by the oracle restatement oracle/sync_protocol.py.
     Nothing from the reference is stored: only inputs and the expected reason codes.
+store_sequence.npz — a sequence of updates run through the reference's OWN exec'd
+    `process_light_client_update` (and one `process_light_client_store_force_update`) from two
+    starting stores (next committee known / unknown): per step the accept flag, the validation
+    reason and a summary of the store (finalized / optimistic slot, best update, committees, max
+    participants).  `python tests/golden/make_golden.py store` regenerates only this file.
 bls_vectors.npz — hash_to_G2 outputs, G1/G2 decompression cases (valid, identity, bad flags, x >= p,
     not on curve, not in the subgroup) and FastAggregateVerify verdicts, all from oracle/bls12_381.py.
 """
@@ -203,6 +208,67 @@ def main():
     make_bls_vectors()
 
 
+# ----------------------------------------------------------------------------- store sequences
+STORE_KINDS = [synth.K_LOW_PARTICIPATION, synth.K_LOW_PARTICIPATION, synth.K_VALID, synth.K_BAD_SIG_MESSAGE,
+               synth.K_LOW_PARTICIPATION, synth.K_VALID, synth.K_BAD_FINALITY_BRANCH, synth.K_VALID,
+               synth.K_LOW_PARTICIPATION, synth.K_VALID, synth.K_BAD_NSC_BRANCH, synth.K_VALID]
+
+
+def store_summary(store) -> list:
+    """Everything process_light_client_update can change, as integers (committees as a digest)."""
+    import hashlib
+    from lcv import layout as L
+
+    def dig(sc):
+        return int.from_bytes(hashlib.sha256(L.pack_sync_committee(sc)).digest()[:7], "little")
+    best = store.best_valid_update
+    return [int(store.finalized_header.beacon.slot), int(store.optimistic_header.beacon.slot),
+            -1 if best is None else int(best.signature_slot), -1 if best is None else int(best.attested_header.beacon.slot),
+            dig(store.current_sync_committee), dig(store.next_sync_committee),
+            int(store.previous_max_active_participants), int(store.current_max_active_participants)]
+
+
+def make_store_sequence():
+    v = H.hostsim_verifier()
+    ns, assert_lines = load_reference()
+    cur, nxt = synth.make_committee(v, 0), synth.make_committee(v, 1)
+    kinds = np.array(STORE_KINDS)
+    sb = synth.generate(v, len(kinds), seed=31, participation="random", kinds=kinds, committees=(cur, nxt))
+    p = sb.updates
+    n = len(kinds)
+    gvr = sb.genesis_validators_root
+    out = {"accepted": [], "reason": [], "summary": []}
+    for next_known in (1, 0):
+        nxt_bytes = nxt.ssz if next_known else bytes(24624)
+        store_r, _ = to_reference_objects(ns, p, 0, sb.store_finalized_slot, cur.ssz, nxt_bytes)
+        acc, rea, summ = [], [], []
+        for i in range(n):
+            _, u_r = to_reference_objects(ns, p, i, sb.store_finalized_slot, cur.ssz, nxt_bytes)
+            rea.append(reference_reason(ns, assert_lines, store_r, u_r, sb.current_slot, gvr))
+            try:
+                ns["process_light_client_update"](store_r, u_r, sb.current_slot, gvr)
+                acc.append(1)
+            except AssertionError:
+                acc.append(0)
+            assert acc[-1] == (rea[-1] == 0)
+            summ.append(store_summary(store_r))
+            print(f"next_known={next_known} step {i:2d} kind {kinds[i]} reason {rea[-1]} store {summ[-1]}", flush=True)
+        force_slot = int(store_r.finalized_header.beacon.slot) + ns["UPDATE_TIMEOUT"] + 1
+        ns["process_light_client_store_force_update"](store_r, force_slot)
+        summ.append(store_summary(store_r))
+        print(f"next_known={next_known} force update at {force_slot}: store {summ[-1]}", flush=True)
+        out["accepted"].append(acc)
+        out["reason"].append(rea)
+        out["summary"].append(summ)
+    np.savez_compressed(os.path.join(HERE, "store_sequence.npz"), **{k: p.__dict__[k] for k in COLS},
+                        nsc_pool=p.nsc_pool, nsc_index=p.nsc_index, signature_slot=p.signature_slot,
+                        store_finalized_slot=np.uint64(sb.store_finalized_slot), current_slot=np.uint64(sb.current_slot),
+                        genesis_validators_root=np.frombuffer(gvr, np.uint8), kinds=kinds,
+                        current_committee=np.frombuffer(cur.ssz, np.uint8), next_committee=np.frombuffer(nxt.ssz, np.uint8),
+                        accepted=np.array(out["accepted"], np.uint8), reason=np.array(out["reason"], np.uint8),
+                        summary=np.array(out["summary"], np.int64))
+
+
 def make_bls_vectors():
     rng = np.random.default_rng(99)
     msgs = [bytes(32), b"\xff" * 32] + [rng.bytes(32) for _ in range(6)]
@@ -257,4 +323,8 @@ def make_bls_vectors():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "store":
+        make_store_sequence()
+    else:
+        main()
+        make_store_sequence()

@@ -109,3 +109,10 @@ def test_validate_large_batch_properties(gpu_verifier):
             assert np.array_equal(r3, reason), shape
     finally:
         gpu_verifier.set_pipeline(1, 1)
+
+
+def test_store_sequence_on_gpu(gpu_verifier):
+    """lcv.store over liblcv.so reproduces the reference's exec'd process_light_client_update
+    sequence (tests/golden/store_sequence.npz) step by step and in the batched form."""
+    import store_cases
+    store_cases.run(gpu_verifier)
