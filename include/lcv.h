@@ -132,6 +132,28 @@ int lcv_fast_aggregate_verify_batch(lcv_ctx* ctx, const uint8_t* committees, uin
 int lcv_merkle_branch_batch(lcv_ctx* ctx, const uint8_t* leaf32, const uint8_t* branch, uint32_t depth,
                             uint64_t index, const uint8_t* root32, uint64_t n, uint8_t* out);
 int lcv_htr_sync_committee_batch(lcv_ctx* ctx, const uint8_t* committees, uint64_t n, uint8_t* roots32_out);
+/* initialize_light_client_store's asserts (sync-protocol.md:353-362), one bootstrap per row (header rows
+ * as lcv_header_cols, committee 24624 B, current_sync_committee_branch 5 x 32 B, trusted_block_root 32 B):
+ * reason 0 ok, 1 header invalid (:353), 2 beacon root != trusted root (:354), 3 committee branch (:356) */
+int lcv_bootstrap_check_batch(lcv_ctx* ctx, const uint8_t* beacon112, const uint8_t* exec832,
+                              const uint8_t* exec_branch128, const uint8_t* committees, const uint8_t* committee_branch160,
+                              const uint8_t* trusted_root32, uint64_t n, uint8_t* reason_out);
+
+/* ---- SSZ wire decode (host only, no device work; csrc/lcv_wire.cpp).  Replaces the upstream SSZ
+ * deserialisation of the reference's containers (sync-protocol.md:109-115 LightClientBootstrap,
+ * :120-133 LightClientUpdate, :138-148 LightClientFinalityUpdate, :153-160 LightClientOptimisticUpdate)
+ * as received over Req/Resp / gossip (p2p-interface.md).  kind: 0 update, 1 finality update,
+ * 2 optimistic update (converted as sync-protocol.md:563-571 / :582-590 do); fork: 0 Deneb
+ * ExecutionPayloadHeader (17 fields), 1 Capella (15).  Message i = buf[offsets[i] .. + lengths[i]] ->
+ * row i of `out` (caller-allocated columns of n rows; out->nsc_pool is ignored).  status[i] = 0 ok,
+ * 1 malformed (row zeroed).  Distinct next_sync_committee values: pool row k is the committee at
+ * buf + pool_src[k] (UINT64_MAX = SyncCommittee()), *npool_out rows (<= n + 1). */
+int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+                           int kind, int fork, const lcv_update_batch* out, uint64_t* pool_src,
+                           uint64_t* npool_out, uint8_t* status);
+int lcv_ssz_decode_bootstrap(const uint8_t* buf, uint64_t len, int fork, uint8_t* beacon112, uint8_t* exec832,
+                             uint8_t* exec_branch128, uint8_t* committee24624, uint8_t* committee_branch160,
+                             uint8_t* status);
 
 /* ---- synthetic-data signer (producer side).  Secret keys 32 B big-endian. */
 int lcv_sk_to_pk_batch(lcv_ctx* ctx, const uint8_t* sk32, uint64_t n, uint8_t* pk48_out);

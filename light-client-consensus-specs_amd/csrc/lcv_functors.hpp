@@ -142,3 +142,31 @@ struct F_import_pq {  // debug pairing inputs: P -> W.pk, Q -> W.qh (no validati
   }
 };
 
+// initialize_light_client_store's checks (sync-protocol.md:353-362), one lane per bootstrap:
+// reason 0 ok, 1 is_valid_light_client_header (:353), 2 hash_tree_root(header.beacon) ==
+// trusted_block_root (:354), 3 current_sync_committee branch (:356-362; CURRENT_SYNC_COMMITTEE_GINDEX
+// 54 -> depth 5, subtree index 22, rooted at header.beacon.state_root)
+struct F_bootstrap {
+  const uint8_t* beacon; const uint8_t* exec; const uint8_t* branch; const uint8_t* sc; const uint8_t* sc_branch;
+  const uint8_t* trusted; uint8_t* out;
+  LCV_HD void operator()(uint32_t i) const {
+    const uint8_t* b = beacon + (size_t)K_BEACON * i;
+    uint8_t r = 0;
+    if (!lc_header_valid(b, exec + (size_t)K_EXEC * i, branch + (size_t)K_EXEC_BRANCH * i)) {
+      r = 1;
+    } else {
+      h256 root, t;
+      htr_beacon(root, b);
+      ld_chunk(t, trusted + 32 * (size_t)i);
+      if (!h256_eq(root, t)) {
+        r = 2;
+      } else {
+        h256 leaf, state;
+        htr_sync_committee(leaf, sc + (size_t)K_SC * i);
+        ld_chunk(state, b + 48);
+        if (!merkle_branch_ok(leaf, sc_branch + 160 * (size_t)i, 5, 22, state)) r = 3;
+      }
+    }
+    out[i] = r;
+  }
+};

@@ -1,0 +1,229 @@
+// SSZ wire decode of light-client messages into the packed SoA rows of include/lcv.h.
+//
+// Containers (reference sync-protocol.md:96-101 LightClientHeader, :120-133 LightClientUpdate,
+// :138-148 LightClientFinalityUpdate, :153-160 LightClientOptimisticUpdate; Req/Resp and gossip
+// payloads p2p-interface.md) in SSZ wire form: fixed parts in field order, 4-byte little-endian
+// offsets for the variable-size fields (every LightClientHeader, because its ExecutionPayloadHeader
+// ends in extra_data: ByteList[32]).  Decoding is strict, as upstream SSZ deserialisation is: the
+// first offset must equal the fixed size, offsets are monotonic and in bounds, no trailing bytes,
+// extra_data <= 32 bytes.  A malformed message yields status 1 and an all-zero row.
+//
+// Finality / optimistic updates become the LightClientUpdate the reference builds from them
+// (sync-protocol.md:563-571 / :582-590): default next_sync_committee, zero next-committee branch,
+// and for optimistic updates a default finalized header and zero finality branch.
+//
+// Distinct next_sync_committee values are deduplicated by content (the device computes
+// HTR(SyncCommittee) once per pool row): pool_src[k] = byte offset in `buf` of pool row k's first
+// occurrence, or UINT64_MAX for SyncCommittee() (all zero).  Pure host code, no device work.
+#include <cstdint>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/lcv.h"
+
+namespace {
+
+constexpr uint64_t kCommittee = 24624, kBeacon = 112, kExecRec = 832, kExecBranch = 128;
+constexpr uint64_t kNscBranch = 160, kFinBranch = 192, kBits = 64, kSig = 96;
+constexpr uint64_t kHeaderFixed = kBeacon + 4 + kExecBranch;  // 244
+constexpr uint64_t kExtraOffPos = 436;                        // extra_data offset inside the exec header
+constexpr uint64_t kMaxExtra = 32;
+
+inline uint32_t rd32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+
+// ExecutionPayloadHeader (Deneb 17 fields / Capella 15) -> 832 B record (layout: include/lcv.h)
+bool decode_exec(const uint8_t* p, uint64_t len, bool deneb, uint8_t* rec) {
+  const uint64_t fixed = deneb ? 584 : 568;
+  if (len < fixed || rd32(p + kExtraOffPos) != fixed) return false;
+  const uint64_t elen = len - fixed;
+  if (elen > kMaxExtra) return false;
+  std::memset(rec, 0, kExecRec);
+  uint64_t o = 0;
+  auto chunk = [&](int leaf, uint64_t n) { std::memcpy(rec + 32 * leaf, p + o, n); o += n; };
+  chunk(0, 32);                                   // parent_hash
+  chunk(1, 20);                                   // fee_recipient
+  chunk(2, 32);                                   // state_root
+  chunk(3, 32);                                   // receipts_root
+  std::memcpy(rec + 544, p + o, 256); o += 256;   // logs_bloom
+  chunk(5, 32);                                   // prev_randao
+  chunk(6, 8); chunk(7, 8); chunk(8, 8); chunk(9, 8);  // block_number, gas_limit, gas_used, timestamp
+  o += 4;                                         // extra_data offset (checked above)
+  chunk(11, 32);                                  // base_fee_per_gas (uint256 LE)
+  chunk(12, 32);                                  // block_hash
+  chunk(13, 32);                                  // transactions_root
+  chunk(14, 32);                                  // withdrawals_root
+  if (deneb) { chunk(15, 8); chunk(16, 8); }      // blob_gas_used, excess_blob_gas
+  std::memcpy(rec + 32 * 10, p + fixed, elen);    // extra_data
+  const uint32_t e32 = (uint32_t)elen;
+  std::memcpy(rec + 800, &e32, 4);
+  return true;
+}
+
+// LightClientHeader: beacon (112) | offset(execution) | execution_branch (128) | execution
+bool decode_header(const uint8_t* p, uint64_t len, bool deneb, uint8_t* beacon, uint8_t* rec, uint8_t* branch) {
+  if (len < kHeaderFixed || rd32(p + kBeacon) != kHeaderFixed) return false;
+  if (!decode_exec(p + kHeaderFixed, len - kHeaderFixed, deneb, rec)) return false;
+  std::memcpy(beacon, p, kBeacon);
+  std::memcpy(branch, p + kBeacon + 4, kExecBranch);
+  return true;
+}
+
+struct Row {
+  const lcv_update_batch* b;
+  uint64_t i;
+  uint8_t* at(const uint8_t* col, uint64_t w) const { return const_cast<uint8_t*>(col) + i * w; }
+};
+
+void zero_row(const Row& r) {
+  const lcv_update_batch* b = r.b;
+  std::memset(r.at(b->attested.beacon, kBeacon), 0, kBeacon);
+  std::memset(r.at(b->attested.execution, kExecRec), 0, kExecRec);
+  std::memset(r.at(b->attested.exec_branch, kExecBranch), 0, kExecBranch);
+  std::memset(r.at(b->finalized.beacon, kBeacon), 0, kBeacon);
+  std::memset(r.at(b->finalized.execution, kExecRec), 0, kExecRec);
+  std::memset(r.at(b->finalized.exec_branch, kExecBranch), 0, kExecBranch);
+  std::memset(r.at(b->nsc_branch, kNscBranch), 0, kNscBranch);
+  std::memset(r.at(b->finality_branch, kFinBranch), 0, kFinBranch);
+  std::memset(r.at(b->sync_bits, kBits), 0, kBits);
+  std::memset(r.at(b->sync_signature, kSig), 0, kSig);
+  const_cast<uint64_t*>(b->signature_slot)[r.i] = 0;
+}
+
+// Decodes one message into row r; *committee = offset (within the message) of next_sync_committee,
+// or UINT64_MAX when the message carries none.
+bool decode_one(const uint8_t* p, uint64_t len, int kind, bool deneb, const Row& r, uint64_t* committee) {
+  const lcv_update_batch* b = r.b;
+  *committee = UINT64_MAX;
+  uint64_t fixed, att_off_pos, fin_off_pos = 0, pos;
+  if (kind == 0) fixed = 4 + kCommittee + kNscBranch + 4 + kFinBranch + kBits + kSig + 8;  // 25152
+  else if (kind == 1) fixed = 4 + 4 + kFinBranch + kBits + kSig + 8;                       // 368
+  else fixed = 4 + kBits + kSig + 8;                                                       // 172
+  if (len < fixed || rd32(p) != fixed) return false;
+  att_off_pos = 0;
+  pos = 4;
+  if (kind == 0) {
+    *committee = pos;
+    pos += kCommittee;
+    std::memcpy(r.at(b->nsc_branch, kNscBranch), p + pos, kNscBranch);
+    pos += kNscBranch;
+  }
+  if (kind != 2) {
+    fin_off_pos = pos;
+    pos += 4;
+    std::memcpy(r.at(b->finality_branch, kFinBranch), p + pos, kFinBranch);
+    pos += kFinBranch;
+  }
+  std::memcpy(r.at(b->sync_bits, kBits), p + pos, kBits);
+  pos += kBits;
+  std::memcpy(r.at(b->sync_signature, kSig), p + pos, kSig);
+  pos += kSig;
+  uint64_t slot;
+  std::memcpy(&slot, p + pos, 8);
+  const_cast<uint64_t*>(b->signature_slot)[r.i] = slot;
+  const uint64_t a0 = rd32(p + att_off_pos);
+  const uint64_t a1 = kind == 2 ? len : rd32(p + fin_off_pos);
+  if (a1 < a0 || a1 > len) return false;
+  if (!decode_header(p + a0, a1 - a0, deneb, r.at(b->attested.beacon, kBeacon),
+                     r.at(b->attested.execution, kExecRec), r.at(b->attested.exec_branch, kExecBranch)))
+    return false;
+  if (kind != 2 &&
+      !decode_header(p + a1, len - a1, deneb, r.at(b->finalized.beacon, kBeacon),
+                     r.at(b->finalized.execution, kExecRec), r.at(b->finalized.exec_branch, kExecBranch)))
+    return false;
+  return true;
+}
+
+// content hash of a committee (64-bit multiply-xor over 8-byte words; collisions resolved by memcmp)
+uint64_t committee_hash(const uint8_t* p) {
+  uint64_t h = 0x9e3779b97f4a7c15ull;
+  for (uint64_t k = 0; k < kCommittee; k += 8) {
+    uint64_t w;
+    std::memcpy(&w, p + k, 8);
+    h = (h ^ w) * 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+  }
+  return h;
+}
+
+bool all_zero(const uint8_t* p, uint64_t n) {
+  for (uint64_t k = 0; k < n; ++k)
+    if (p[k]) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths,
+                                      uint64_t n, int kind, int fork, const lcv_update_batch* out,
+                                      uint64_t* pool_src, uint64_t* npool_out, uint8_t* status) {
+  if ((n && (!buf || !offsets || !lengths || !out || !pool_src || !status)) || !npool_out) return LCV_EINVAL;
+  if (kind < 0 || kind > 2 || fork < 0 || fork > 1) return LCV_EINVAL;
+  if (n && (!out->attested.beacon || !out->attested.execution || !out->attested.exec_branch ||
+            !out->finalized.beacon || !out->finalized.execution || !out->finalized.exec_branch ||
+            !out->nsc_index || !out->nsc_branch || !out->finality_branch || !out->sync_bits ||
+            !out->sync_signature || !out->signature_slot))
+    return LCV_EINVAL;
+  const bool deneb = fork == 0;
+  std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
+  uint64_t npool = 0;
+  int zero_row_ix = -1;  // pool row of SyncCommittee(), created on first use
+  uint32_t* nsc_index = const_cast<uint32_t*>(out->nsc_index);
+  for (uint64_t i = 0; i < n; ++i) {
+    const Row r{out, i};
+    zero_row(r);
+    uint64_t c = UINT64_MAX;
+    const bool ok = decode_one(buf + offsets[i], lengths[i], kind, deneb, r, &c);
+    status[i] = ok ? 0 : 1;
+    if (!ok) {
+      zero_row(r);
+      c = UINT64_MAX;
+    }
+    const uint8_t* cp = c == UINT64_MAX ? nullptr : buf + offsets[i] + c;
+    if (!cp || all_zero(cp, kCommittee)) {
+      if (zero_row_ix < 0) {
+        zero_row_ix = (int)npool;
+        pool_src[npool++] = UINT64_MAX;
+      }
+      nsc_index[i] = (uint32_t)zero_row_ix;
+      continue;
+    }
+    std::vector<uint32_t>& cands = seen[committee_hash(cp)];
+    int hit = -1;
+    for (uint32_t k : cands)
+      if (std::memcmp(buf + pool_src[k], cp, kCommittee) == 0) { hit = (int)k; break; }
+    if (hit < 0) {
+      hit = (int)npool;
+      pool_src[npool++] = offsets[i] + c;
+      cands.push_back((uint32_t)hit);
+    }
+    nsc_index[i] = (uint32_t)hit;
+  }
+  *npool_out = npool;
+  return LCV_OK;
+}
+
+// LightClientBootstrap (sync-protocol.md:109-115): header (offset) | current_sync_committee (24624) |
+// current_sync_committee_branch (5 x 32) | header.  Input of initialize_light_client_store (:351-373).
+extern "C" int lcv_ssz_decode_bootstrap(const uint8_t* buf, uint64_t len, int fork, uint8_t* beacon112,
+                                        uint8_t* exec832, uint8_t* exec_branch128, uint8_t* committee24624,
+                                        uint8_t* committee_branch160, uint8_t* status) {
+  if (!buf || !beacon112 || !exec832 || !exec_branch128 || !committee24624 || !committee_branch160 || !status)
+    return LCV_EINVAL;
+  if (fork < 0 || fork > 1) return LCV_EINVAL;
+  constexpr uint64_t fixed = 4 + kCommittee + kNscBranch;  // 24788
+  bool ok = len >= fixed && rd32(buf) == fixed &&
+            decode_header(buf + fixed, len - fixed, fork == 0, beacon112, exec832, exec_branch128);
+  if (ok) {
+    std::memcpy(committee24624, buf + 4, kCommittee);
+    std::memcpy(committee_branch160, buf + 4 + kCommittee, kNscBranch);
+  } else {
+    std::memset(beacon112, 0, kBeacon);
+    std::memset(exec832, 0, kExecRec);
+    std::memset(exec_branch128, 0, kExecBranch);
+    std::memset(committee24624, 0, kCommittee);
+    std::memset(committee_branch160, 0, kNscBranch);
+  }
+  *status = ok ? 0 : 1;
+  return LCV_OK;
+}

@@ -226,6 +226,23 @@ class Verifier:
                     "lcv_htr_sync_committee_batch")
         return out
 
+    def bootstrap_check_batch(self, beacon: np.ndarray, execution: np.ndarray, exec_branch: np.ndarray,
+                              committees: np.ndarray, committee_branch: np.ndarray, trusted_roots: np.ndarray
+                              ) -> np.ndarray:
+        """initialize_light_client_store's asserts (sync-protocol.md:353-362) per row -> reason codes
+        (0 ok, 1 header, 2 trusted root, 3 current_sync_committee branch)."""
+        beacon = np.ascontiguousarray(beacon, np.uint8).reshape(-1, 112)
+        n = beacon.shape[0]
+        cols = [beacon, np.ascontiguousarray(execution, np.uint8).reshape(n, EXEC_RECORD_BYTES),
+                np.ascontiguousarray(exec_branch, np.uint8).reshape(n, 128),
+                np.ascontiguousarray(committees, np.uint8).reshape(n, SYNC_COMMITTEE_BYTES),
+                np.ascontiguousarray(committee_branch, np.uint8).reshape(n, 160),
+                np.ascontiguousarray(trusted_roots, np.uint8).reshape(n, 32)]
+        out = np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_bootstrap_check_batch(self.ctx, *[ptr(c) for c in cols], n, ptr(out)),
+                    "lcv_bootstrap_check_batch")
+        return out
+
     def sk_to_pk_batch(self, sks: np.ndarray) -> np.ndarray:
         sks = np.ascontiguousarray(sks, np.uint8).reshape(-1, 32)
         out = np.zeros((sks.shape[0], 48), np.uint8)

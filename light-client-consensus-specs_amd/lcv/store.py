@@ -9,6 +9,8 @@ Host restatement of the reference's store logic, driven by the batched HIP verif
     process_light_client_update             sync-protocol.md:508-553
     process_light_client_finality_update    sync-protocol.md:559-573
     process_light_client_optimistic_update  sync-protocol.md:578-592
+    initialize_light_client_store           sync-protocol.md:351-373 (its three asserts run in the
+                                            HIP kernel F_bootstrap)
 
 plus `process_light_client_updates(store, updates, current_slot, gvr)`: the reference's sequential
 loop `for u in updates: process_light_client_update(store, u, ...)` (an AssertionError rejects the
@@ -24,12 +26,14 @@ containers, or the lightweight defaults below for the finality / optimistic conv
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from types import SimpleNamespace
-from typing import Optional, Sequence
+from typing import Any, Optional, Sequence
 
 import numpy as np
 
 from . import layout as L
+from . import runtime
 from .device import Verifier
 from .sync_protocol import REASONS, validate_light_client_updates
 
@@ -237,3 +241,46 @@ def process_light_client_optimistic_update(store, optimistic_update, current_slo
     """sync-protocol.md:578-592."""
     process_light_client_update(store, _optimistic_as_update(optimistic_update), current_slot,
                                 genesis_validators_root, verifier)
+
+
+# ------------------------------------------------------------------ bootstrap (sync-protocol.md:164-179, :351-373)
+@dataclass
+class LightClientStore:
+    """sync-protocol.md:164-179 (field names and meaning as the reference's dataclass)."""
+    finalized_header: Any
+    current_sync_committee: Any
+    next_sync_committee: Any
+    best_valid_update: Optional[Any]
+    optimistic_header: Any
+    previous_max_active_participants: int
+    current_max_active_participants: int
+
+
+BOOTSTRAP_REASONS = {
+    0: ("", "valid"),
+    1: ("sync-protocol.md:353", "is_valid_light_client_header(bootstrap.header)"),
+    2: ("sync-protocol.md:354", "hash_tree_root(bootstrap.header.beacon) == trusted_block_root"),
+    3: ("sync-protocol.md:356-362", "is_valid_merkle_branch(current_sync_committee_branch)"),
+}
+
+
+def initialize_light_client_store(trusted_block_root: bytes, bootstrap, verifier: Optional[Verifier] = None
+                                  ) -> LightClientStore:
+    """sync-protocol.md:351-373: the header-validity, trusted-root and committee-branch asserts run on the
+    device (lcv_bootstrap_check_batch); raises AssertionError naming the failing assert."""
+    v = verifier if verifier is not None else runtime.default_verifier()
+    beacon, execution, branch = L.pack_header(bootstrap.header)
+    root = bytes(trusted_block_root)
+    if len(root) != 32:
+        raise ValueError("trusted_block_root must be 32 bytes")
+    u8 = lambda b: np.frombuffer(b, np.uint8)  # noqa: E731
+    r = int(v.bootstrap_check_batch(u8(beacon), u8(execution), u8(branch),
+                                    u8(L.pack_sync_committee(bootstrap.current_sync_committee)),
+                                    u8(L.pack_branch(bootstrap.current_sync_committee_branch, 5)), u8(root))[0])
+    if r:
+        line, what = BOOTSTRAP_REASONS[r]
+        raise AssertionError(f"initialize_light_client_store: assert {what} failed ({line}, reason {r})")
+    return LightClientStore(finalized_header=bootstrap.header, current_sync_committee=bootstrap.current_sync_committee,
+                            next_sync_committee=_default_sync_committee(), best_valid_update=None,
+                            optimistic_header=bootstrap.header, previous_max_active_participants=0,
+                            current_max_active_participants=0)

@@ -1,0 +1,139 @@
+"""SSZ wire decode of light-client messages straight into the packed batch.
+
+Light-client data reaches a client as SSZ bytes (Req/Resp `LightClientUpdatesByRange` chunks,
+`light_client_finality_update` / `light_client_optimistic_update` gossip, `LightClientBootstrap`;
+p2p-interface.md).  Upstream, each message is deserialised into Python containers
+(sync-protocol.md:109-115, :120-133, :138-148, :153-160) and then validated one at a time.  Here a
+whole batch of messages is decoded by the native decoder of liblcv.so (`lcv_ssz_decode_updates`,
+csrc/lcv_wire.cpp: host C++, strict SSZ offset rules) directly into the `PackedUpdates` rows the
+device verifier consumes; no per-update Python objects are built.
+
+    decode_updates(messages, kind="update", fork="deneb")  -> PackedUpdates   (ValueError if malformed)
+    decode_updates_status(messages, kind, fork)             -> (PackedUpdates, ok: np.ndarray[bool])
+    decode_bootstrap(data, fork="deneb")                    -> Bootstrap (header rows, committee, branch)
+
+`kind` "finality" / "optimistic" rows are the LightClientUpdate the reference builds from those
+messages (sync-protocol.md:563-571 / :582-590).  `messages` is a sequence of `bytes`, or a tuple
+(buf: uint8 array, offsets: uint64 array, lengths: uint64 array) describing messages inside one
+buffer (e.g. a received Req/Resp payload, without copying).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import layout as L
+from ._native import HeaderCols, Lib, UpdateBatch, load, ptr
+from .device import PackedUpdates
+
+KINDS = {"update": 0, "finality": 1, "optimistic": 2}
+FORKS = {"deneb": 0, "capella": 1}
+
+Messages = Union[Sequence[bytes], Tuple[np.ndarray, np.ndarray, np.ndarray]]
+
+
+def _lib(lib: Optional[Lib]) -> Lib:
+    return lib if lib is not None else load()
+
+
+def _flatten(messages: Messages) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    if isinstance(messages, tuple) and len(messages) == 3 and isinstance(messages[0], np.ndarray):
+        buf, offs, lens = messages
+        buf = np.ascontiguousarray(buf, np.uint8).reshape(-1)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        if offs.shape != lens.shape or (offs.size and int((offs + lens).max()) > buf.size):
+            raise ValueError("offsets/lengths do not describe messages inside buf")
+        return buf, offs, lens
+    parts = [bytes(m) for m in messages]
+    lens = np.array([len(p) for p in parts], np.uint64)
+    offs = np.zeros(len(parts), np.uint64)
+    if len(parts):
+        offs[1:] = np.cumsum(lens)[:-1]
+    buf = np.frombuffer(b"".join(parts), np.uint8) if parts else np.zeros(0, np.uint8)
+    return buf, offs, lens
+
+
+def decode_updates_status(messages: Messages, kind: str = "update", fork: str = "deneb",
+                          lib: Optional[Lib] = None) -> Tuple[PackedUpdates, np.ndarray]:
+    """Decode n SSZ messages -> (PackedUpdates, ok); malformed messages give all-zero rows, ok False."""
+    if kind not in KINDS or fork not in FORKS:
+        raise ValueError(f"kind must be one of {list(KINDS)}, fork one of {list(FORKS)}")
+    buf, offs, lens = _flatten(messages)
+    n = int(offs.size)
+    cols = {k: np.zeros((n, w), np.uint8) for k, w in (
+        ("att_beacon", L.BEACON_BYTES), ("att_exec", L.EXEC_BYTES), ("att_branch", L.EXEC_BRANCH_BYTES),
+        ("fin_beacon", L.BEACON_BYTES), ("fin_exec", L.EXEC_BYTES), ("fin_branch", L.EXEC_BRANCH_BYTES),
+        ("nsc_branch", L.NSC_BRANCH_BYTES), ("finality_branch", L.FINALITY_BRANCH_BYTES),
+        ("sync_bits", L.BITS_BYTES), ("sync_signature", L.SIGNATURE_BYTES))}
+    nsc_index = np.zeros(n, np.uint32)
+    sig_slot = np.zeros(n, np.uint64)
+    pool_src = np.zeros(n + 1, np.uint64)
+    npool = C.c_uint64(0)
+    status = np.zeros(max(n, 1), np.uint8)
+    b = UpdateBatch()
+    b.attested = HeaderCols(ptr(cols["att_beacon"]), ptr(cols["att_exec"]), ptr(cols["att_branch"]))
+    b.finalized = HeaderCols(ptr(cols["fin_beacon"]), ptr(cols["fin_exec"]), ptr(cols["fin_branch"]))
+    b.nsc_index = ptr(nsc_index, C.c_uint32)
+    b.nsc_branch = ptr(cols["nsc_branch"])
+    b.finality_branch = ptr(cols["finality_branch"])
+    b.sync_bits = ptr(cols["sync_bits"])
+    b.sync_signature = ptr(cols["sync_signature"])
+    b.signature_slot = ptr(sig_slot, C.c_uint64)
+    b.n = n
+    b.npool = 0
+    src = buf if buf.size else np.zeros(1, np.uint8)
+    rc = _lib(lib).lcv_ssz_decode_updates(ptr(src), ptr(offs, C.c_uint64), ptr(lens, C.c_uint64), n, KINDS[kind],
+                                         FORKS[fork], C.byref(b), ptr(pool_src, C.c_uint64), C.byref(npool),
+                                         ptr(status))
+    if rc != 0:
+        raise ValueError(f"lcv_ssz_decode_updates: status {rc}")
+    k = int(npool.value)
+    pool = np.zeros((max(k, 1), L.SYNC_COMMITTEE_BYTES), np.uint8)
+    for j in range(k):  # distinct committees only: a handful per batch
+        s = int(pool_src[j])
+        if s != 0xFFFFFFFFFFFFFFFF:
+            pool[j] = buf[s:s + L.SYNC_COMMITTEE_BYTES]
+    batch = PackedUpdates(nsc_pool=pool, nsc_index=nsc_index, signature_slot=sig_slot, **cols)
+    return batch, status[:n] == 0
+
+
+def decode_updates(messages: Messages, kind: str = "update", fork: str = "deneb",
+                   lib: Optional[Lib] = None) -> PackedUpdates:
+    """Strict decode: raises ValueError (as upstream SSZ deserialisation does) if any message is malformed."""
+    batch, ok = decode_updates_status(messages, kind, fork, lib)
+    if not ok.all():
+        bad = np.flatnonzero(~ok)
+        raise ValueError(f"malformed SSZ {kind} message(s) at index {bad[:8].tolist()}")
+    return batch
+
+
+@dataclass
+class Bootstrap:
+    """LightClientBootstrap (sync-protocol.md:109-115) as packed rows (layouts of include/lcv.h)."""
+    beacon: np.ndarray                 # (112,) u8
+    execution: np.ndarray              # (832,) u8 execution record
+    execution_branch: np.ndarray       # (128,) u8
+    current_sync_committee: np.ndarray  # (24624,) u8
+    current_sync_committee_branch: np.ndarray  # (160,) u8
+
+
+def decode_bootstrap(data: bytes, fork: str = "deneb", lib: Optional[Lib] = None) -> Bootstrap:
+    if fork not in FORKS:
+        raise ValueError(f"fork must be one of {list(FORKS)}")
+    buf = np.frombuffer(bytes(data), np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = Bootstrap(np.zeros(L.BEACON_BYTES, np.uint8), np.zeros(L.EXEC_BYTES, np.uint8),
+                    np.zeros(L.EXEC_BRANCH_BYTES, np.uint8), np.zeros(L.SYNC_COMMITTEE_BYTES, np.uint8),
+                    np.zeros(L.NSC_BRANCH_BYTES, np.uint8))
+    st = np.zeros(1, np.uint8)
+    rc = _lib(lib).lcv_ssz_decode_bootstrap(ptr(buf), len(data), FORKS[fork], ptr(out.beacon), ptr(out.execution),
+                                           ptr(out.execution_branch), ptr(out.current_sync_committee),
+                                           ptr(out.current_sync_committee_branch), ptr(st))
+    if rc != 0:
+        raise ValueError(f"lcv_ssz_decode_bootstrap: status {rc}")
+    if st[0]:
+        raise ValueError("malformed SSZ LightClientBootstrap")
+    return out

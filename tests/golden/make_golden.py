@@ -17,6 +17,10 @@ store_sequence.npz — a sequence of updates run through the reference's OWN exe
     starting stores (next committee known / unknown): per step the accept flag, the validation
     reason and a summary of the store (finalized / optimistic slot, best update, committees, max
     participants).  `python tests/golden/make_golden.py store` regenerates only this file.
+wire.npz — SSZ wire bytes produced by the reference's OWN exec'd containers (LightClientUpdate,
+    LightClientFinalityUpdate, LightClientOptimisticUpdate, LightClientBootstrap) from golden rows, and
+    bootstrap cases whose expected reason is the failing assert of the reference's exec'd
+    `initialize_light_client_store`.  `python tests/golden/make_golden.py wire` regenerates only this.
 bls_vectors.npz — hash_to_G2 outputs, G1/G2 decompression cases (valid, identity, bad flags, x >= p,
     not on curve, not in the subgroup) and FastAggregateVerify verdicts, all from oracle/bls12_381.py.
 """
@@ -322,9 +326,106 @@ def make_bls_vectors():
     print("bls vectors:", len(msgs), "h2c,", len(sigs), "signature decodings")
 
 
+# ----------------------------------------------------------------------------- SSZ wire + bootstrap
+WIRE_UPDATE_ROWS = (0, 6, 21, 22, 28, 30)   # full updates: Deneb, bad nsc branch, no finality, no nsc, capella, bellatrix
+
+
+def _bootstrap_assert_lines():
+    text = open(REF).read()
+    for m in re.finditer(r"```python\n(.*?)```", text, re.S):
+        if m.group(1).startswith("def initialize_light_client_store"):
+            start_line = text[:m.start(1)].count("\n") + 1
+            tree = ast.parse("\n" * (start_line - 1) + m.group(1))
+            return sorted((n.lineno, n.end_lineno) for n in ast.walk(tree) if isinstance(n, ast.Assert))
+    raise RuntimeError("initialize_light_client_store not found")
+
+
+def make_wire():
+    import hashlib
+    from oracle.ssz import serialize
+    from golden_cases import load_updates
+    from lcv.device import PackedUpdates
+    ns, _ = load_reference()
+    g = load_updates()
+    p = PackedUpdates(nsc_pool=g["nsc_pool"], nsc_index=g["nsc_index"], signature_slot=g["signature_slot"],
+                      **{k: g[k] for k in COLS})
+    n = len(g["expected_reason"])
+    LCH, LCU = ns["LightClientHeader"], ns["LightClientUpdate"]
+    LCF, LCO, LCB = ns["LightClientFinalityUpdate"], ns["LightClientOptimisticUpdate"], ns["LightClientBootstrap"]
+    msgs, kind, row = [], [], []
+
+    def put(obj, k, i):
+        b = serialize(obj)
+        assert serialize(type(obj).de(b)) == b  # the reference container round-trips its own bytes
+        msgs.append(b); kind.append(k); row.append(i)
+
+    for i in range(n):
+        _, u = to_reference_objects(ns, p, i, 0, bytes(24624), bytes(24624))
+        if i in WIRE_UPDATE_ROWS:
+            put(u, 0, i)
+        put(LCF(attested_header=u.attested_header, finalized_header=u.finalized_header, finality_branch=u.finality_branch,
+                sync_aggregate=u.sync_aggregate, signature_slot=u.signature_slot), 1, i)
+        put(LCO(attested_header=u.attested_header, sync_aggregate=u.sync_aggregate, signature_slot=u.signature_slot), 2, i)
+    # bootstraps: header = a golden attested header whose state_root commits to a committee at
+    # CURRENT_SYNC_COMMITTEE_GINDEX (54: depth 5, subtree index 22) through a synthetic branch
+    rng = np.random.default_rng(54)
+    cur, nxt = g["nsc_pool"][0].tobytes(), g["nsc_pool"][1].tobytes()
+    lines = _bootstrap_assert_lines()
+    assert len(lines) == 3, lines
+    B_cases = [("deneb_valid", 0, {}), ("capella_valid", 28, {}), ("bellatrix_valid", 30, {}),
+               ("bad_execution_branch", 0, {"exec_branch": True}), ("capella_blob_gas", 29, {}),
+               ("wrong_trusted_root", 0, {"trusted": True}), ("bad_committee_branch", 0, {"branch": True}),
+               ("other_committee", 28, {"committee": True}), ("bellatrix_bad_committee_branch", 30, {"branch": True})]
+    bmsgs, btrusted, breason, bnames = [], [], [], []
+    sha = lambda b: hashlib.sha256(b).digest()  # noqa: E731
+    for name, i, over in B_cases:
+        _, u = to_reference_objects(ns, p, i, 0, bytes(24624), bytes(24624))
+        h = u.attested_header
+        branch = [rng.bytes(32) for _ in range(5)]
+        node = bytes(S.hash_tree_root(H.committee_from(cur)))
+        for d in range(5):
+            node = sha(branch[d] + node) if (22 >> d) & 1 else sha(node + branch[d])
+        h.beacon.state_root = node
+        if over.get("exec_branch"):
+            eb = list(h.execution_branch); eb[2] = flip(bytes(eb[2]), 7); h.execution_branch = eb
+        if over.get("branch"):
+            branch[3] = flip(branch[3], 30)
+        trusted = bytes(S.hash_tree_root(h.beacon))
+        if over.get("trusted"):
+            trusted = flip(trusted, 0)
+        bs = LCB(header=h, current_sync_committee=H.committee_from(nxt if over.get("committee") else cur),
+                 current_sync_committee_branch=branch)
+        import traceback
+        try:
+            ns["initialize_light_client_store"](trusted, bs)
+            r = 0
+        except AssertionError:
+            tb = [f.lineno for f in traceback.extract_tb(sys.exc_info()[2]) if f.filename == "sync-protocol.md"]
+            r = next(k for k, (a, b) in enumerate(lines) if a <= tb[-1] <= b) + 1
+        b = serialize(bs)
+        assert serialize(LCB.de(b)) == b
+        bmsgs.append(b); btrusted.append(trusted); breason.append(r); bnames.append(name)
+        print(f"bootstrap {name:32s} reason {r}", flush=True)
+    offs = np.cumsum([0] + [len(m) for m in msgs])
+    boffs = np.cumsum([0] + [len(m) for m in bmsgs])
+    np.savez_compressed(os.path.join(HERE, "wire.npz"),
+                        buf=np.frombuffer(b"".join(msgs), np.uint8), offsets=offs[:-1].astype(np.uint64),
+                        lengths=np.diff(offs).astype(np.uint64), kind=np.array(kind, np.uint8), row=np.array(row, np.uint32),
+                        boot_buf=np.frombuffer(b"".join(bmsgs), np.uint8), boot_offsets=boffs[:-1].astype(np.uint64),
+                        boot_lengths=np.diff(boffs).astype(np.uint64),
+                        boot_trusted=np.frombuffer(b"".join(btrusted), np.uint8).reshape(-1, 32),
+                        boot_reason=np.array(breason, np.uint8))
+    json.dump({"bootstrap_cases": bnames, "bootstrap_reason": breason, "reference_assert_lines": lines,
+               "messages": len(msgs)}, open(os.path.join(HERE, "wire.json"), "w"), indent=1)
+    print("wire:", len(msgs), "messages,", len(bmsgs), "bootstraps")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "store":
         make_store_sequence()
+    elif len(sys.argv) > 1 and sys.argv[1] == "wire":
+        make_wire()
     else:
         main()
         make_store_sequence()
+        make_wire()
