@@ -161,6 +161,7 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
+    wire_out = wire_path(v, sb, args.n)
     total = world * args.n * args.steps
     stage_avg = {k: round(ms / args.steps, 3) for k, ms in stage_ms.items()}
     kernel_ms = sum(stage_avg.values())
@@ -192,6 +193,7 @@ def main():
         "serial_stage_ms_per_step": stage_avg,
         "pcie_inclusive_updates_per_s_1gpu": round(pcie_rate, 1),
         "roofline": roof,
+        "wire": wire_out,
     }
     if not args.no_cpu_baseline and world == 1:
         try:
@@ -202,6 +204,34 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def wire_path(v, sb, n: int) -> dict:
+    """SSZ wire path, beside `value`: the batch serialised to LightClientUpdate
+    SSZ bytes, decoded by the native decoder (host threads) and validated from host buffers; the
+    decoded rows must reproduce the packed batch exactly (full-size round trip)."""
+    from lcv import wire
+    msgs = wire.encode_updates(sb.updates)
+    buf = np.frombuffer(b"".join(msgs), np.uint8)
+    lens = np.array([len(m) for m in msgs], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    wire.decode_updates(msgs[:1])  # binds the library outside the timed decode
+    t0 = time.perf_counter()
+    wb = wire.decode_updates((buf, offs, lens))
+    t_dec = time.perf_counter() - t0
+    ok, _ = v.validate(wb, sb.current_slot, sb.genesis_validators_root)
+    t_all = time.perf_counter() - t0
+    u = sb.updates
+    same = all(np.array_equal(getattr(wb, k), getattr(u, k)) for k in (
+        "att_beacon", "att_exec", "att_branch", "fin_beacon", "fin_exec", "fin_branch", "nsc_branch",
+        "finality_branch", "sync_bits", "sync_signature", "signature_slot"))
+    pairs = np.unique(np.stack([wb.nsc_index, u.nsc_index], 1), axis=0)
+    same = same and all(np.array_equal(wb.nsc_pool[a], u.nsc_pool[b]) for a, b in pairs)
+    return {"bytes": int(buf.nbytes), "decode_updates_per_s": round(n / t_dec, 1),
+            "decode_gb_per_s": round(buf.nbytes / t_dec / 1e9, 2),
+            "decode_plus_validate_updates_per_s_1gpu": round(n / t_all, 1),
+            "roundtrip_exact": bool(same), "all_valid": bool(ok.all()),
+            "host_threads": min(16, os.cpu_count() or 1)}
 
 
 def total_ops_per_update():

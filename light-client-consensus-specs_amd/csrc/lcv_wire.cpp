@@ -17,6 +17,7 @@
 // occurrence, or UINT64_MAX for SyncCommittee() (all zero).  Pure host code, no device work.
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -134,22 +135,49 @@ bool decode_one(const uint8_t* p, uint64_t len, int kind, bool deneb, const Row&
   return true;
 }
 
-// content hash of a committee (64-bit multiply-xor over 8-byte words; collisions resolved by memcmp)
-uint64_t committee_hash(const uint8_t* p) {
+// Dedup key of a committee: a hash of its first pubkey and its aggregate_pubkey (96 sampled bytes);
+// every key hit is confirmed by a full 24,624-byte compare, so the sample only has to spread rows.
+uint64_t committee_key(const uint8_t* p) {
   uint64_t h = 0x9e3779b97f4a7c15ull;
-  for (uint64_t k = 0; k < kCommittee; k += 8) {
-    uint64_t w;
-    std::memcpy(&w, p + k, 8);
-    h = (h ^ w) * 0xff51afd7ed558ccdull;
-    h ^= h >> 29;
-  }
+  auto mix = [&](const uint8_t* q) {
+    for (int k = 0; k < 48; k += 8) {
+      uint64_t w;
+      std::memcpy(&w, q + k, 8);
+      h = (h ^ w) * 0xff51afd7ed558ccdull;
+      h ^= h >> 29;
+    }
+  };
+  mix(p);
+  mix(p + kCommittee - 48);
   return h;
 }
 
-bool all_zero(const uint8_t* p, uint64_t n) {
-  for (uint64_t k = 0; k < n; ++k)
-    if (p[k]) return false;
+bool all_zero(const uint8_t* p, uint64_t n) {  // n multiple of 8
+  for (uint64_t k = 0; k < n; k += 512) {
+    uint64_t acc = 0;
+    const uint64_t e = k + 512 < n ? k + 512 : n;
+    for (uint64_t j = k; j < e; j += 8) {
+      uint64_t w;
+      std::memcpy(&w, p + j, 8);
+      acc |= w;
+    }
+    if (acc) return false;
+  }
   return true;
+}
+
+// rows are independent: split [0, n) over host threads (the batch path; small batches stay inline)
+template <class Fn> void parallel_rows(uint64_t n, Fn fn) {
+  unsigned t = std::thread::hardware_concurrency();
+  t = t < 1 ? 1 : (t > 16 ? 16 : t);
+  if (n < 1024 || t == 1) { fn(0, n); return; }
+  std::vector<std::thread> pool;
+  const uint64_t step = (n + t - 1) / t;
+  for (unsigned k = 0; k < t; ++k) {
+    const uint64_t lo = k * step, hi = lo + step < n ? lo + step : n;
+    if (lo < hi) pool.emplace_back(fn, lo, hi);
+  }
+  for (auto& th : pool) th.join();
 }
 
 }  // namespace
@@ -165,38 +193,56 @@ extern "C" int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offset
             !out->sync_signature || !out->signature_slot))
     return LCV_EINVAL;
   const bool deneb = fork == 0;
+  constexpr uint64_t kNone = UINT64_MAX;
+  std::vector<uint64_t> csrc(n, kNone), key(n, 0);  // committee offset in buf (kNone: SyncCommittee())
+  // 1. decode every row (parallel)
+  parallel_rows(n, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      const Row r{out, i};
+      zero_row(r);
+      uint64_t c = kNone;
+      const bool ok = decode_one(buf + offsets[i], lengths[i], kind, deneb, r, &c);
+      status[i] = ok ? 0 : 1;
+      if (!ok) {
+        zero_row(r);
+        continue;
+      }
+      if (c != kNone && !all_zero(buf + offsets[i] + c, kCommittee)) {
+        csrc[i] = offsets[i] + c;
+        key[i] = committee_key(buf + csrc[i]);
+      }
+    }
+  });
+  // 2. pool rows in first-occurrence order; each row tentatively takes the first pool row of its key
+  uint32_t* nsc_index = const_cast<uint32_t*>(out->nsc_index);
   std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
   uint64_t npool = 0;
-  int zero_row_ix = -1;  // pool row of SyncCommittee(), created on first use
-  uint32_t* nsc_index = const_cast<uint32_t*>(out->nsc_index);
+  int64_t zero_ix = -1;  // pool row of SyncCommittee(), created on first use
   for (uint64_t i = 0; i < n; ++i) {
-    const Row r{out, i};
-    zero_row(r);
-    uint64_t c = UINT64_MAX;
-    const bool ok = decode_one(buf + offsets[i], lengths[i], kind, deneb, r, &c);
-    status[i] = ok ? 0 : 1;
-    if (!ok) {
-      zero_row(r);
-      c = UINT64_MAX;
-    }
-    const uint8_t* cp = c == UINT64_MAX ? nullptr : buf + offsets[i] + c;
-    if (!cp || all_zero(cp, kCommittee)) {
-      if (zero_row_ix < 0) {
-        zero_row_ix = (int)npool;
-        pool_src[npool++] = UINT64_MAX;
-      }
-      nsc_index[i] = (uint32_t)zero_row_ix;
+    if (csrc[i] == kNone) {
+      if (zero_ix < 0) { zero_ix = (int64_t)npool; pool_src[npool++] = kNone; }
+      nsc_index[i] = (uint32_t)zero_ix;
       continue;
     }
-    std::vector<uint32_t>& cands = seen[committee_hash(cp)];
-    int hit = -1;
+    std::vector<uint32_t>& cands = seen[key[i]];
+    if (cands.empty()) { cands.push_back((uint32_t)npool); pool_src[npool++] = csrc[i]; }
+    nsc_index[i] = cands[0];
+  }
+  // 3. confirm every tentative assignment with a full compare (parallel)
+  std::vector<uint8_t> mismatch(n, 0);
+  parallel_rows(n, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i)
+      if (csrc[i] != kNone && pool_src[nsc_index[i]] != csrc[i])
+        mismatch[i] = std::memcmp(buf + pool_src[nsc_index[i]], buf + csrc[i], kCommittee) != 0;
+  });
+  // 4. sampled-key collisions (distinct committees sharing first and aggregate pubkeys): exact search
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!mismatch[i]) continue;
+    std::vector<uint32_t>& cands = seen[key[i]];
+    int64_t hit = -1;
     for (uint32_t k : cands)
-      if (std::memcmp(buf + pool_src[k], cp, kCommittee) == 0) { hit = (int)k; break; }
-    if (hit < 0) {
-      hit = (int)npool;
-      pool_src[npool++] = offsets[i] + c;
-      cands.push_back((uint32_t)hit);
-    }
+      if (std::memcmp(buf + pool_src[k], buf + csrc[i], kCommittee) == 0) { hit = k; break; }
+    if (hit < 0) { hit = (int64_t)npool; cands.push_back((uint32_t)npool); pool_src[npool++] = csrc[i]; }
     nsc_index[i] = (uint32_t)hit;
   }
   *npool_out = npool;

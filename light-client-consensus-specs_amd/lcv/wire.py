@@ -11,6 +11,7 @@ device verifier consumes; no per-update Python objects are built.
     decode_updates(messages, kind="update", fork="deneb")  -> PackedUpdates   (ValueError if malformed)
     decode_updates_status(messages, kind, fork)             -> (PackedUpdates, ok: np.ndarray[bool])
     decode_bootstrap(data, fork="deneb")                    -> Bootstrap (header rows, committee, branch)
+    encode_updates(batch, kind="update", fork="deneb")      -> [bytes]  (serving side; inverse of decode)
 
 `kind` "finality" / "optimistic" rows are the LightClientUpdate the reference builds from those
 messages (sync-protocol.md:563-571 / :582-590).  `messages` is a sequence of `bytes`, or a tuple
@@ -136,4 +137,43 @@ def decode_bootstrap(data: bytes, fork: str = "deneb", lib: Optional[Lib] = None
         raise ValueError(f"lcv_ssz_decode_bootstrap: status {rc}")
     if st[0]:
         raise ValueError("malformed SSZ LightClientBootstrap")
+    return out
+
+
+# ------------------------------------------------------------------ encode (serving side)
+_EXEC_SPANS = ((0, 32), (32, 52), (64, 96), (96, 128), (544, 800), (160, 192), (192, 200), (224, 232), (256, 264),
+               (288, 296), None, (352, 384), (384, 416), (416, 448), (448, 480), (480, 488), (512, 520))
+
+
+def _encode_header(beacon: np.ndarray, rec: np.ndarray, branch: np.ndarray, fork: str) -> bytes:
+    elen = int.from_bytes(rec[800:804].tobytes(), "little")
+    spans = _EXEC_SPANS if fork == "deneb" else _EXEC_SPANS[:15]
+    fixed = 584 if fork == "deneb" else 568
+    ex = b"".join(fixed.to_bytes(4, "little") if s is None else rec[s[0]:s[1]].tobytes() for s in spans)
+    return (beacon.tobytes() + (L.BEACON_BYTES + 4 + L.EXEC_BRANCH_BYTES).to_bytes(4, "little") + branch.tobytes()
+            + ex + rec[320:320 + elen].tobytes())
+
+
+def encode_updates(batch: PackedUpdates, kind: str = "update", fork: str = "deneb") -> list:
+    """Packed rows -> SSZ wire bytes of LightClientUpdate / FinalityUpdate / OptimisticUpdate (the
+    inverse of decode_updates for rows that came from such messages; a full node serves these)."""
+    if kind not in KINDS or fork not in FORKS:
+        raise ValueError(f"kind must be one of {list(KINDS)}, fork one of {list(FORKS)}")
+    out = []
+    for i in range(batch.n):
+        att = _encode_header(batch.att_beacon[i], batch.att_exec[i], batch.att_branch[i], fork)
+        tail = batch.sync_bits[i].tobytes() + batch.sync_signature[i].tobytes() + int(batch.signature_slot[i]).to_bytes(8, "little")
+        if kind == "optimistic":
+            fixed = 4 + len(tail)
+            out.append(fixed.to_bytes(4, "little") + tail + att)
+            continue
+        fin = _encode_header(batch.fin_beacon[i], batch.fin_exec[i], batch.fin_branch[i], fork)
+        mid = batch.finality_branch[i].tobytes() + tail
+        if kind == "finality":
+            fixed = 8 + len(mid)
+            out.append(fixed.to_bytes(4, "little") + (fixed + len(att)).to_bytes(4, "little") + mid + att + fin)
+            continue
+        sc = batch.nsc_pool[int(batch.nsc_index[i])].tobytes() + batch.nsc_branch[i].tobytes()
+        fixed = 4 + len(sc) + 4 + len(mid)
+        out.append(fixed.to_bytes(4, "little") + sc + (fixed + len(att)).to_bytes(4, "little") + mid + att + fin)
     return out

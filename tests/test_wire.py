@@ -246,3 +246,28 @@ def test_decode_then_validate_gpu(gpu_verifier, kind):
     assert got.tolist() == exp.tolist()
     if kind == 0:
         assert got.tolist() == g["expected_reason"][rows].tolist()
+
+
+def test_dedup_exact_on_sampled_key_collision():
+    """Committees equal in the sampled bytes (first + aggregate pubkey) but different elsewhere stay
+    distinct pool rows; identical ones share a row; a large batch takes the threaded path."""
+    w = load_wire()
+    full = messages(w, [int(np.flatnonzero(w["kind"] == 0)[0])])[0]
+    other = bytearray(full)
+    other[4 + 48 * 100 + 5] ^= 0x01   # committee starts at byte 4: pubkey 100 differs
+    msgs = ([full, bytes(other)] * 700)[:1400]
+    for lib in libs():
+        batch = wire.decode_updates(msgs, lib=lib)
+        assert batch.nsc_pool.shape[0] == 2
+        assert batch.nsc_index[0::2].tolist() == [0] * 700 and batch.nsc_index[1::2].tolist() == [1] * 700
+        assert batch.nsc_pool[1].tobytes() == bytes(other[4:4 + 24624])
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_encode_reproduces_reference_bytes(kind):
+    """encode_updates(decode_updates(x)) == x for the reference-serialised messages."""
+    w = load_wire()
+    msgs = messages(w, np.flatnonzero(w["kind"] == kind))
+    k = ["update", "finality", "optimistic"][kind]
+    batch = wire.decode_updates(msgs, kind=k, lib=libs()[0])
+    assert wire.encode_updates(batch, kind=k) == msgs
