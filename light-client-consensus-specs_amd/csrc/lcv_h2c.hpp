@@ -115,12 +115,20 @@ LCV_FN void sswu_e2prime(fp2& xo, fp2& yo, const fp2& u) {
   const bool sq1 = fp2_is_square_alpha(gx1, alpha);
   fp2_sel(x, sq1, x1, x2);
   fp2_sel(gx, sq1, gx1, gx2);
-  if (!sq1) {
-    fp n;
-    fp2_norm(n, gx2);
-    fp_pow_p1d4(alpha, n);
-  }
-  fp2_sqrt_alpha(y, gx, alpha);
+  // gx1 not a square: gx2 = (Z u^2)^3 gx1, hence norm(gx2)^((p+1)/4) = +-norm(Z)^(3(p+1)/4) norm(u)^3 alpha
+  // (fp2_sqrt_alpha accepts either sign).  Four multiplications replace a second 381-bit exponentiation
+  // that a wave would otherwise run whenever any of its lanes takes this branch.  (The exceptional
+  // den0 case has gx1 square by the choice of Z, RFC 9380 §6.6.2, so it never reads alpha2.)
+  fp nu, alpha2, c2;
+  fp2_norm(nu, u);
+  fp_sqr(alpha2, nu);
+  fp_mul(alpha2, alpha2, nu);
+  LCV_FP_SET(c2, LCV_SSWU_ALPHA2_C_INIT);
+  fp_mul(alpha2, alpha2, c2);
+  fp_mul(alpha2, alpha2, alpha);
+  fp alpha_sel;
+  fp_sel(alpha_sel, sq1, alpha, alpha2);
+  fp2_sqrt_alpha(y, gx, alpha_sel);
   if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
   xo = x;
   yo = y;
