@@ -45,7 +45,7 @@ struct F_eng_g2sub {
 // interpreter's term loops and reductions branch on SGPRs.  Blocks are one wave, so the barrier
 // between rounds is a wave barrier (LDS operations of one wave complete in order).
 template <class F>
-__global__ __launch_bounds__(64) void k_eng(F f, uint32_t n) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_eng(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
   static_assert(lcv::ENG_REC_WORDS == 8, "lane record = two 16-byte loads");
   __shared__ uint32_t lds[F::SHARED_WORDS + G * F::LDS_WORDS];

@@ -990,7 +990,7 @@ def emit(progs, path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--team", type=int, default=16)
+    ap.add_argument("--team", type=int, default=32, help="Miller team (32: 720 rounds vs 1,070 at 16; r01_v12)")
     ap.add_argument("--fexp-team", type=int, default=16)
     ap.add_argument("--g2-team", type=int, default=16)
     ap.add_argument("--check", action="store_true")
