@@ -120,9 +120,11 @@ int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
 int lcv_last_timings(lcv_ctx* ctx, float* ms_out, int max_stages, int* nstages);
 const char* lcv_stage_name(int stage);
 
-/* ---- bls.FastAggregateVerify (sync-protocol.md:464); py_ecc semantics (every key KeyValidated) */
-int lcv_fast_aggregate_verify(lcv_ctx* ctx, const uint8_t* pubkeys48, uint64_t npk, const uint8_t* msg32,
-                              const uint8_t* sig96, int* result);
+/* ---- bls.FastAggregateVerify (sync-protocol.md:464); py_ecc semantics (every key KeyValidated).
+ * Any number of pubkeys (npk = 0 -> False), a message of any length (the light-client call site passes
+ * a 32-byte signing root; other lengths take the device's byte-streamed expand_message_xmd). */
+int lcv_fast_aggregate_verify(lcv_ctx* ctx, const uint8_t* pubkeys48, uint64_t npk, const uint8_t* msg,
+                              uint64_t msg_len, const uint8_t* sig96, int* result);
 /* batched: committee table (ncomm x 512 x 48 B), per item committee id + participation bits */
 int lcv_fast_aggregate_verify_batch(lcv_ctx* ctx, const uint8_t* committees, uint64_t ncomm,
                                     const uint32_t* committee_id, const uint8_t* bits64, const uint8_t* msg32,
@@ -162,6 +164,8 @@ int lcv_sign_batch(lcv_ctx* ctx, const uint8_t* sk32, const uint8_t* msg32, uint
 /* ---- parity-test entry points (intermediate values, canonical big-endian bytes) */
 /* field ops on (a, b) < p: out per item = a*b, a+b, a-b, a^-1, sqrt_fp2(a + b u) (2 x 48); ok = sqrt exists */
 int lcv_debug_fp(lcv_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint64_t n, uint8_t* out288, uint8_t* ok);
+/* a^((p+1)/4) || a^((p-3)/4) (2 x 48 B) for a < p: the windowed sqrt exponentiations of decompression / SSWU */
+int lcv_debug_fp_pow(lcv_ctx* ctx, const uint8_t* a48, uint64_t n, uint8_t* out96);
 /* hash_to_G2(msg) affine (x0 || x1 || y0 || y1, 4 x 48 B); inf flag */
 int lcv_debug_hash_to_g2(lcv_ctx* ctx, const uint8_t* msg32, uint64_t n, uint8_t* out192, uint8_t* inf);
 /* signature decode + subgroup check: affine point + status (0 ok, 1 identity, 2 invalid) */

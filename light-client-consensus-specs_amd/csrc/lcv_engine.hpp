@@ -28,6 +28,7 @@ struct ProgView {
   const uint32_t* consts;  // 12 limbs per constant (Montgomery), copied into LDS slots nslots..
   uint32_t rounds;
   uint32_t nslots, nconst;
+  uint32_t zero;           // slot of the zero constant (record padding terms read it)
 };
 enum { ENG_REC_WORDS = LCV_PROG_REC_HW / 2 };
 
@@ -126,18 +127,40 @@ LCV_FN void eng_eval(fp& out, const uint32_t* w, uint32_t n, uint32_t maxc, uint
 }
 
 // one round for one lane: record w (ENG_REC_WORDS words), header h0/h1 (wave-uniform)
-LCV_FN void eng_exec(const uint32_t* w, uint32_t h0, uint32_t h1, uint32_t* lds, const uint32_t* cl, uint32_t ns) {
+LCV_FN void eng_exec(const uint32_t* w, uint32_t h0, uint32_t h1, uint32_t* lds, const uint32_t* cl, uint32_t ns,
+                     uint32_t zero) {
+  (void)zero;
   const uint32_t nA = h0 & 0xFu, mA = (h0 >> 4) & 0xFu, kA = (h0 >> 8) & 7u, loA = (h0 >> 11) & 1u ? 0u : 1u;
   const uint32_t nB = (h0 >> 12) & 0xFu, mB = (h0 >> 16) & 0xFu, kB = (h0 >> 20) & 7u;
   const uint32_t dst = eng_hw(w, 0);
   fp a;
   eng_eval<1, LCV_PROG_KLIN>(a, w, nA, mA, kA, loA, lds, cl, ns);
+#if defined(LCV_HOSTSIM)
+  // host simulation: only the lanes that own a MUL multiply (the device runs the product in every
+  // lane of a MUL round and discards it), so the op counter sees the program's algorithmic work:
+  // one Fp multiplication per MUL op, (terms - 1) Fp additions per combination
+  if ((dst & 0xFFFu) != ENG_SLOT_NONE) {
+    auto terms = [&](int base, uint32_t n) {  // the lane's own terms (padding reads the zero constant)
+      uint32_t t = 0;
+      for (uint32_t k = 0; k < n; ++k) t += (eng_hw(w, base + (int)k) & 0xFFFu) != zero;
+      return t;
+    };
+    for (uint32_t k = 1; k < terms(1, nA); ++k) LCV_COUNT(1);
+    if ((h1 & 0x100u) && (dst & ENG_MUL)) {
+      for (uint32_t k = 1; k < terms(LCV_PROG_B_AT, nB); ++k) LCV_COUNT(1);
+      fp b;
+      eng_eval<LCV_PROG_B_AT, LCV_PROG_REC_HW - LCV_PROG_B_AT>(b, w, nB, mB, kB, 1u, lds, cl, ns);
+      fp_mul(a, a, b);
+    }
+  }
+#else
   if (h1 & 0x100u) {  // a MUL round (B operands have <= 4 terms); LIN lanes keep A
     fp b, m;
     eng_eval<LCV_PROG_B_AT, LCV_PROG_REC_HW - LCV_PROG_B_AT>(b, w, nB, mB, kB, 1u, lds, cl, ns);
     fp_mul(m, a, b);
     if (dst & ENG_MUL) a = m;
   }
+#endif
   if (h1 & 0x200u) {
     if (dst & ENG_INV) fp_inv_bingcd(a, a);
   }
@@ -147,7 +170,7 @@ LCV_FN void eng_exec(const uint32_t* w, uint32_t h0, uint32_t h1, uint32_t* lds,
 // one round of a program for lane `lane` (host simulation and the generic round loop)
 LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t team, uint32_t* lds, const uint32_t* cl) {
   const uint32_t* w = P.rec + ((size_t)r * team + lane) * ENG_REC_WORDS;
-  eng_exec(w, P.hdr[2 * r], P.hdr[2 * r + 1], lds, cl, P.nslots);
+  eng_exec(w, P.hdr[2 * r], P.hdr[2 * r + 1], lds, cl, P.nslots, P.zero);
 }
 
 }  // namespace lcv

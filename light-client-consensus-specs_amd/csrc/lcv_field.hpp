@@ -323,14 +323,18 @@ LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
   x1.v[0] = 1;
   fp_zero(x2);
   while (!raw_is_one(u) && !raw_is_one(v)) {
+    // op counter: each shift + modular halving, and each subtraction pair, is two Fp additions' work
     while ((u.v[0] & 1u) == 0) {
+      LCV_COUNT(1); LCV_COUNT(1);
       raw_shr1(u);
       raw_half_mod(x1);
     }
     while ((v.v[0] & 1u) == 0) {
+      LCV_COUNT(1); LCV_COUNT(1);
       raw_shr1(v);
       raw_half_mod(x2);
     }
+    LCV_COUNT(1); LCV_COUNT(1);
     if (!raw_sub(t, u, v)) {  // u >= v
       u = t;
       raw_sub_mod(x1, x1, x2);

@@ -16,6 +16,7 @@ struct F_pre { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operato
 struct F_h2c_map { Work W; LCV_HD void operator()(uint32_t t) const { item_h2c_map(t, W); } };
 struct F_sig { BatchDev B; Work W; LCV_HD void operator()(uint32_t i) const { item_sig(i, B, W); } };
 struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32_t i) const { item_agg(i, B, C, W); } };
+struct F_agg_fold { Work W; uint32_t m; LCV_HD void operator()(uint32_t) const { item_agg_fold(m, W); } };
 struct F_verdict { Work W; LCV_HD void operator()(uint32_t i) const { item_verdict(i, W); } };
 struct F_key { CommitteeDev C; LCV_HD void operator()(uint32_t t) const { item_committee_key(t, C); } };
 struct F_sum { CommitteeDev C; LCV_HD void operator()(uint32_t c) const { item_committee_sum(c, C); } };
@@ -26,6 +27,14 @@ struct F_msg_import {  // 32-byte messages -> W.msg (big-endian words, SoA)
     h256 m;
     LCV_UNROLL for (int k = 0; k < 8; ++k) m.w[k] = ld_be32(msg + 32 * (size_t)i + 4 * k);
     soa_st_h256(W.msg, W.cap, i, m);
+  }
+};
+struct F_msg_import_b0 {  // one message of any length -> expand_message_xmd's b0 in W.msg (W.msg_b0 = 1)
+  const uint8_t* msg; uint64_t len; Work W;
+  LCV_HD void operator()(uint32_t i) const {
+    h256 b0;
+    xmd_b0_bytes(b0, msg, len);
+    soa_st_h256(W.msg, W.cap, i, b0);
   }
 };
 struct F_merkle {
@@ -93,6 +102,16 @@ struct F_dbg_fp {
     fp_to_be48(o + 192, y.c0);
     fp_to_be48(o + 240, y.c1);
     ok[i] = s ? 1 : 0;
+  }
+};
+struct F_dbg_pow {  // the sqrt-candidate exponentiations (sliding window, fp_pow_p1d4 / fp_pow_p3d4)
+  const uint8_t* a48; uint8_t* out;
+  LCV_HD void operator()(uint32_t i) const {
+    fp a, r;
+    fp_from_be48_mont(a, a48 + 48 * (size_t)i);
+    uint8_t* o = out + 96 * (size_t)i;
+    fp_pow_p1d4(r, a); fp_to_be48(o, r);
+    fp_pow_p3d4(r, a); fp_to_be48(o + 48, r);
   }
 };
 struct F_export_g2 {  // SoA affine G2 -> canonical bytes

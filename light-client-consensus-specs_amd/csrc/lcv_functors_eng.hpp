@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
       q1 = rec[o + 1];
       h = hdr[r + 1];
     }
-    if (active) lcv::eng_exec(w, h0, h1, my, lds, ns);
+    if (active) lcv::eng_exec(w, h0, h1, my, lds, ns, 0u);
     __syncthreads();
   }
   if (active) f(item, lane, R + 1, my, lds);

@@ -144,6 +144,55 @@ LCV_FN void map_to_curve_g2(g2j& r, const fp2& u) {
 }
 
 // hash_to_field(msg, 2)[m] (RFC 9380 §5.2; u_1 needs the xmd chain through u_0's blocks)
+// b0 of expand_message_xmd for a message of any length: SHA-256(Z_pad || msg || I2OSP(256, 2) ||
+// I2OSP(0, 1) || DST || I2OSP(43, 1)), streamed byte by byte after the constant Z_pad midstate
+// (FastAggregateVerify drop-in with a message that is not a 32-byte signing root; one lane per message)
+LCV_FN void xmd_b0_bytes(h256& b0, const uint8_t* msg, uint64_t len) {
+  constexpr uint32_t H1[8] = LCV_XMD_H1_INIT;
+  const char* dst = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
+  uint32_t st[8], blk[16];
+  LCV_UNROLL for (int k = 0; k < 8; ++k) st[k] = H1[k];
+  const uint64_t body = len + 47;                 // msg || 01 00 || 00 || DST (43) || 2b
+  const uint64_t total = (body + 9 + 63) / 64 * 64;  // + 0x80 + 64-bit bit length, whole blocks
+  const uint64_t bits = (64 + body) * 8;          // Z_pad included in the message length
+  LCV_NOUNROLL for (uint64_t base = 0; base < total; base += 64) {
+    LCV_NOUNROLL for (int w = 0; w < 16; ++w) {
+      uint32_t word = 0;
+      for (int b = 0; b < 4; ++b) {
+        const uint64_t k = base + 4 * w + b;
+        uint32_t byte;
+        if (k < len) byte = msg[k];
+        else if (k == len) byte = 0x01;
+        else if (k < len + 3) byte = 0x00;
+        else if (k < len + 46) byte = (uint8_t)dst[k - len - 3];
+        else if (k == len + 46) byte = 43;
+        else if (k == body) byte = 0x80;
+        else if (k >= total - 8) byte = (uint32_t)(bits >> (8 * (total - 1 - k))) & 0xFFu;
+        else byte = 0;
+        word = (word << 8) | byte;
+      }
+      blk[w] = word;
+    }
+    sha256_compress(st, blk);
+  }
+  LCV_UNROLL for (int k = 0; k < 8; ++k) b0.w[k] = st[k];
+}
+
+// u_m from a given b0 (the rest of expand_message_xmd + hash_to_field)
+LCV_FN void hash_to_field_u_b0(fp2& u, const h256& b0, uint32_t m) {
+  h256 prev, hi, lo;
+  h256_zero(prev);
+  LCV_NOUNROLL for (uint32_t k = 0; k <= m; ++k) {
+    xmd_next(hi, b0, prev, 4 * k + 1);
+    xmd_next(lo, b0, hi, 4 * k + 2);
+    fp_from_xmd64(u.c0, hi, lo);
+    xmd_next(hi, b0, lo, 4 * k + 3);
+    xmd_next(lo, b0, hi, 4 * k + 4);
+    fp_from_xmd64(u.c1, hi, lo);
+    prev = lo;
+  }
+}
+
 LCV_FN void hash_to_field_u(fp2& u, const h256& msg, uint32_t m) {
   h256 b0, prev, hi, lo;
   xmd_b0(b0, msg);

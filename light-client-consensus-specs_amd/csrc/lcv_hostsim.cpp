@@ -18,10 +18,13 @@ struct lcv_ctx;
 namespace lcv { std::atomic<unsigned long long> g_ops[3]; }
 #endif
 
+// Stage marks are kept per (simulated) stream, like the HIP backend's, so that marks opened on
+// different streams never overwrite each other; the driver's marks do not nest on one stream.
 struct Backend {
-  int open_stage = -1;
-  std::chrono::steady_clock::time_point t0;
-  unsigned long long ops0[3] = {0, 0, 0};
+  int cur = 0;
+  int open_stage[4] = {-1, -1, -1, -1};
+  std::chrono::steady_clock::time_point t0[4];
+  unsigned long long ops0[4][3] = {};
   unsigned long long ops[16][3] = {};
 };
 
@@ -38,7 +41,7 @@ template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
 static int be_fork(lcv_ctx*) { return 0; }
 static int be_join(lcv_ctx*) { return 0; }
-static void be_use_stream(lcv_ctx*, int) {}
+static void be_use_stream(lcv_ctx* ctx, int k);
 static int be_fork_to(lcv_ctx*, int) { return 0; }
 static int be_join_from(lcv_ctx*, int) { return 0; }
 static int be_nstreams() { return 4; }
@@ -81,23 +84,27 @@ template <class F> static int be_launch_team(lcv_ctx*, const F& f, uint32_t n) {
   }
   return LCV_OK;
 }
+static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = (k > 0 && k < 4) ? k : 0; }
 static void be_stage_begin(lcv_ctx* ctx, int stage) {
-  ctx->be.open_stage = stage;
-  ctx->be.t0 = std::chrono::steady_clock::now();
+  Backend& b = ctx->be;
+  b.open_stage[b.cur] = stage;
+  b.t0[b.cur] = std::chrono::steady_clock::now();
 #ifdef LCV_OPCOUNT
-  for (int k = 0; k < 3; ++k) ctx->be.ops0[k] = lcv::g_ops[k].load();
+  for (int k = 0; k < 3; ++k) b.ops0[b.cur][k] = lcv::g_ops[k].load();
 #endif
 }
 static void be_stage_end(lcv_ctx* ctx, int stage) {
-  if (ctx->be.open_stage != stage) return;
+  Backend& b = ctx->be;
+  if (b.open_stage[b.cur] != stage) return;
   const auto t1 = std::chrono::steady_clock::now();
-  ctx->stage_ms[stage] += std::chrono::duration<float, std::milli>(t1 - ctx->be.t0).count();
+  ctx->stage_ms[stage] += std::chrono::duration<float, std::milli>(t1 - b.t0[b.cur]).count();
 #ifdef LCV_OPCOUNT
-  for (int k = 0; k < 3; ++k) ctx->be.ops[stage][k] += lcv::g_ops[k].load() - ctx->be.ops0[k];
+  for (int k = 0; k < 3; ++k) b.ops[stage][k] += lcv::g_ops[k].load() - b.ops0[b.cur][k];
 #endif
-  ctx->be.open_stage = -1;
+  b.open_stage[b.cur] = -1;
 }
 static void be_reset_timings(lcv_ctx* ctx) {
+  for (int k = 0; k < 4; ++k) ctx->be.open_stage[k] = -1;
   for (int s = 0; s < ST_COUNT; ++s) ctx->stage_ms[s] = 0.f;
   for (int s = 0; s < 16; ++s) for (int k = 0; k < 3; ++k) ctx->be.ops[s][k] = 0;
 }

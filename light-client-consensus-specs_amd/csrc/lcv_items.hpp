@@ -76,6 +76,7 @@ struct Work {
   uint8_t* pair_ok;      // [cap]
   uint8_t* verdict;      // [cap]
   uint8_t* reason;       // [cap]
+  uint32_t msg_b0;       // 1: W.msg already holds expand_message_xmd's b0 (arbitrary-length messages)
 };
 
 // ---- SoA helpers
@@ -259,7 +260,8 @@ LCV_FN void item_h2c_map(uint32_t t, const Work& W) {
   h256 msg;
   soa_ld_h256(msg, W.msg, W.cap, i);
   fp2 u, x, y;
-  hash_to_field_u(u, msg, m);
+  if (W.msg_b0) hash_to_field_u_b0(u, msg, m);
+  else hash_to_field_u(u, msg, m);
   sswu_e2prime(x, y, u);
   soa_st_fp2(W.qmap, W.cap, i, 2 * m, x);
   soa_st_fp2(W.qmap, W.cap, i, 2 * m + 1, y);
@@ -318,6 +320,29 @@ LCV_FN void item_agg(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
   soa_st_fp(W.pk, W.cap, i, 0, a.x);
   soa_st_fp(W.pk, W.cap, i, 1, a.y);
   W.agg_status[i] = (uint8_t)(anybad ? PT_BAD : (inf || pc == 0 ? PT_INF : PT_OK));
+}
+
+// FastAggregateVerify with more keys than one 512-key table: items 0..m-1 hold the masked aggregates
+// of consecutive 512-key slices of the caller's list; item 0 becomes their sum (any invalid key ->
+// PT_BAD, an identity sum -> PT_INF).  One lane; m = ceil(npk / 512) is small.
+LCV_FN void item_agg_fold(uint32_t m, const Work& W) {
+  g1j acc;
+  jac_set_inf(acc);
+  bool bad = false;
+  for (uint32_t k = 0; k < m; ++k) {
+    if (W.agg_status[k] == PT_BAD) bad = true;
+    if (W.agg_status[k] != PT_OK) continue;
+    g1a p;
+    soa_ld_fp(p.x, W.pk, W.cap, k, 0);
+    soa_ld_fp(p.y, W.pk, W.cap, k, 1);
+    jac_madd(acc, acc, p);
+  }
+  const bool inf = jac_is_inf(acc);
+  g1a a;
+  jac_to_aff(a, acc);
+  soa_st_fp(W.pk, W.cap, 0, 0, a.x);
+  soa_st_fp(W.pk, W.cap, 0, 1, a.y);
+  W.agg_status[0] = (uint8_t)(bad ? PT_BAD : (inf ? PT_INF : PT_OK));
 }
 
 LCV_FN void item_verdict(uint32_t i, const Work& W) {

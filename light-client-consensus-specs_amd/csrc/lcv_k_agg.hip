@@ -5,4 +5,5 @@
 #include "lcv_functors.hpp"
 
 LCV_INSTANTIATE(F_agg)
+LCV_INSTANTIATE(F_agg_fold)
 LCV_INSTANTIATE(F_sum)

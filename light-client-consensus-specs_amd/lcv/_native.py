@@ -64,7 +64,7 @@ SIGNATURES = {
     "lcv_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
     "lcv_set_pipeline": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "lcv_stage_name": (C.c_char_p, [C.c_int]),
-    "lcv_fast_aggregate_verify": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, u8p, C.POINTER(C.c_int)]),
+    "lcv_fast_aggregate_verify": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, C.c_uint64, u8p, C.POINTER(C.c_int)]),
     "lcv_fast_aggregate_verify_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u32p, u8p, u8p, u8p, C.c_uint64, u8p]),
     "lcv_merkle_branch_batch": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint32, C.c_uint64, u8p, C.c_uint64, u8p]),
     "lcv_htr_sync_committee_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p]),
@@ -75,6 +75,7 @@ SIGNATURES = {
     "lcv_sk_to_pk_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p]),
     "lcv_sign_batch": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint64, u8p]),
     "lcv_debug_fp": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint64, u8p, u8p]),
+    "lcv_debug_fp_pow": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p]),
     "lcv_debug_hash_to_g2": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, u8p]),
     "lcv_debug_g2_decompress": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, u8p]),
     "lcv_debug_aggregate": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u32p, u8p, C.c_uint64, u8p, u8p]),

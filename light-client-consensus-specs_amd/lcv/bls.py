@@ -28,14 +28,11 @@ def FastAggregateVerify(pubkeys: Sequence[bytes], message: bytes, signature: byt
         msg, sig = bytes(message), bytes(signature)
     except Exception:
         return False
-    if len(pks) == 0 or len(msg) != 32 or len(sig) != 96 or any(len(p) != 48 for p in pks):
+    if len(pks) == 0 or len(sig) != 96 or any(len(p) != 48 for p in pks):
         return False
     v = verifier if verifier is not None else runtime.default_verifier()
-    if len(pks) <= 512:
-        return v.fast_aggregate_verify(pks, msg, sig)
-    # more keys than one committee table: split into tables of 512, aggregate on device per table
-    # is not expressible through the ABI; the light-client path never needs it (512-member committees)
-    raise ValueError("FastAggregateVerify: at most 512 pubkeys per call are supported")
+    # any key count (tables of 512 keys, slice aggregates summed on device) and any message length
+    return v.fast_aggregate_verify(pks, msg, sig)
 
 
 def FastAggregateVerifyBatch(committees: np.ndarray, committee_id: np.ndarray, bits: np.ndarray, messages: np.ndarray,

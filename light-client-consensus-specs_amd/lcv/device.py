@@ -185,10 +185,11 @@ class Verifier:
         if any(len(bytes(p)) != 48 for p in pubkeys):
             return False
         msg, sig = bytes(message), bytes(signature)
-        if len(msg) != 32 or len(sig) != 96:
+        if len(sig) != 96:
             return False
+        m = as_u8(msg) if msg else np.zeros(1, np.uint8)
         res = C.c_int()
-        self._check(self.lib.lcv_fast_aggregate_verify(self.ctx, ptr(pks), len(pubkeys), ptr(as_u8(msg)),
+        self._check(self.lib.lcv_fast_aggregate_verify(self.ctx, ptr(pks), len(pubkeys), ptr(m), len(msg),
                                                        ptr(as_u8(sig)), C.byref(res)), "lcv_fast_aggregate_verify")
         return bool(res.value)
 
@@ -265,6 +266,13 @@ class Verifier:
         ok = np.zeros(n, np.uint8)
         self._check(self.lib.lcv_debug_fp(self.ctx, ptr(a), ptr(b), n, ptr(out), ptr(ok)), "lcv_debug_fp")
         return out, ok
+
+    def debug_fp_pow(self, a: np.ndarray) -> np.ndarray:
+        """(n, 96): a^((p+1)/4) || a^((p-3)/4), canonical big-endian."""
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1, 48)
+        out = np.zeros((a.shape[0], 96), np.uint8)
+        self._check(self.lib.lcv_debug_fp_pow(self.ctx, ptr(a), a.shape[0], ptr(out)), "lcv_debug_fp_pow")
+        return out
 
     def debug_hash_to_g2(self, msgs: np.ndarray):
         msgs = np.ascontiguousarray(msgs, np.uint8).reshape(-1, 32)

@@ -205,16 +205,26 @@ def _header(rng, slot: int):
 
 def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERIOD, participation: str = "full",
              kinds: Optional[np.ndarray] = None, with_next: bool = True, with_finality: bool = True,
-             committees=None, gvr: Optional[bytes] = None, sign_next: bool = False) -> SyntheticBatch:
+             committees=None, gvr: Optional[bytes] = None, sign_next: bool = False, npool: int = 1) -> SyntheticBatch:
     """n synthetic updates against one store (finalized at the first slot of `period`, both
     committees known).  participation: "full" (512/512) or "random" (popcount uniform in [342,512]).
     kinds: optional per-row corruption kinds (see K_*).  sign_next: signature slots in the next period,
-    signed by the next committee (sync-protocol.md:452-455 selects it)."""
+    signed by the next committee (sync-protocol.md:452-455 selects it).  npool > 1 (BASELINE configs[3],
+    the SHA-256-heavy form): update i carries next_sync_committee number i % npool out of npool
+    distinct committees (HTR(SyncCommittee), 1,025 SHA-256 calls, then runs once per distinct value);
+    the store's next committee is then unknown, as :441-442 would otherwise demand equality with it."""
     rng = np.random.default_rng(seed)
     cur, nxt = committees if committees is not None else (make_committee(verifier, 0), make_committee(verifier, 1))
     gvr = gvr if gvr is not None else sha256(b"lcv-synthetic-genesis-validators-root")
     kinds = np.zeros(n, np.int64) if kinds is None else np.asarray(kinds, np.int64)
     store_fin = period * SLOTS_PER_PERIOD
+    if npool > 1:
+        if sign_next:
+            raise ValueError("npool > 1 needs the store's next committee unknown (no next-period signing)")
+        prng = np.random.default_rng(seed + 1000)
+        pool_bytes = prng.integers(0, 256, (npool, L.SYNC_COMMITTEE_BYTES), dtype=np.uint8)
+        pool_roots = [bytes(r) for r in verifier.htr_sync_committee_batch(pool_bytes)]
+        store_next = Committee([], bytes(512 * 48), bytes(48))  # is_next_sync_committee_known: False
     nsc_root = htr_sync_committee(nxt.ssz)
     cur_root = htr_sync_committee(cur.ssz)
     signer = nxt if sign_next else cur
@@ -244,7 +254,7 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
         else:
             f_ex, f_br, f_beacon, fin_leaf = bytes(832), bytes(128), bytes(112), None
         n104, n53, n12, n7, n2 = (rng.bytes(32) for _ in range(5))
-        n55 = nsc_root if with_next else rng.bytes(32)
+        n55 = (pool_roots[i % npool] if npool > 1 else nsc_root) if with_next else rng.bytes(32)
         n27 = sha256(cur_root + n55)
         if with_finality:
             n52 = sha256(n104 + fin_leaf)
@@ -306,11 +316,29 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
         sigs[i, 0] = 0x9a  # compression flag set, x1 >= p
         sigs[i, 1:48] = 0xff
     cols["sync_signature"][:] = sigs
-    nsc_pool = np.frombuffer(nxt.ssz if with_next else bytes(L.SYNC_COMMITTEE_BYTES), np.uint8).reshape(1, -1).copy()
-    upd = PackedUpdates(nsc_pool=nsc_pool, nsc_index=np.zeros(n, np.uint32), signature_slot=sig_slot, **cols)
+    if npool > 1 and with_next:
+        nsc_pool, nsc_index = pool_bytes, (np.arange(n) % npool).astype(np.uint32)
+    else:
+        nsc_pool = np.frombuffer(nxt.ssz if with_next else bytes(L.SYNC_COMMITTEE_BYTES), np.uint8).reshape(1, -1).copy()
+        nsc_index = np.zeros(n, np.uint32)
+    upd = PackedUpdates(nsc_pool=nsc_pool, nsc_index=nsc_index, signature_slot=sig_slot, **cols)
     expected = np.array([EXPECTED_REASON[int(k)] for k in kinds], np.uint8)
     current_slot = int(sig_slot.max()) if n else store_fin + 1
-    return SyntheticBatch(upd, kinds, expected, store_fin, cur, nxt, current_slot, gvr)
+    return SyntheticBatch(upd, kinds, expected, store_fin, cur, store_next if npool > 1 else nxt, current_slot, gvr)
+
+
+def tile(sb: SyntheticBatch, reps: int) -> SyntheticBatch:
+    """`reps` copies of a generated batch back to back (the 10^6-row configs: rows are independent,
+    so a tiled batch has the same per-row verdicts; generating 10^6 distinct rows on the host would
+    dominate a test's time).  The next-committee pool is shared, not copied."""
+    u = sb.updates
+    cols = {k: np.ascontiguousarray(np.tile(getattr(u, k), (reps, 1))) for k in (
+        "att_beacon", "att_exec", "att_branch", "fin_beacon", "fin_exec", "fin_branch", "nsc_branch",
+        "finality_branch", "sync_bits", "sync_signature")}
+    upd = PackedUpdates(nsc_pool=u.nsc_pool, nsc_index=np.tile(u.nsc_index, reps),
+                        signature_slot=np.tile(u.signature_slot, reps), **cols)
+    return SyntheticBatch(upd, np.tile(sb.kinds, reps), np.tile(sb.expected_reason, reps), sb.store_finalized_slot,
+                          sb.current, sb.next, sb.current_slot, sb.genesis_validators_root)
 
 
 def adversarial_kinds(n: int, seed: int = 5, bad_fraction: float = 0.10) -> np.ndarray:

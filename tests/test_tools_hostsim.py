@@ -1,0 +1,68 @@
+"""CPU checks of the build tooling and of device arithmetic through the host simulation:
+  * tools/gen_programs.py emulates every generated team program (Miller loop, final exponentiation,
+    hash_to_G2 tail, G2 subgroup check) with Python integers against the oracle;
+  * tools/opcount.py (the roofline numerator) attributes work to every BLS stage, one mark per kernel;
+  * the windowed sqrt exponentiations of lcv_field.hpp vs pow() (host simulation of the device code).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+sys.path.insert(0, os.path.join(H.ROOT, "tools"))
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+
+
+def test_generated_programs_match_oracle():
+    import gen_programs as G
+    progs = [G.make_miller(32), G.make_fexp(16), G.make_h2c(16), G.make_g2sub(16)]
+    G.check_miller(progs[0], 32)
+    G.check_fexp(progs[1])
+    G.check_h2c(progs[2])
+    G.check_g2sub(progs[3])
+    # the committed kernel header is what the generator emits now (no stale program ships)
+    inc = os.path.join(H.PKG, "csrc", "lcv_programs.inc")
+    text = open(inc).read()
+    for p in progs:
+        assert f"#define LCV_PROG_{p.name.upper()}_ROUNDS {len(p.rounds)}" in text
+        assert f"#define LCV_PROG_{p.name.upper()}_SLOTS {p.nslots}" in text
+
+
+def test_opcount_every_stage():
+    ops = os.path.join(H.PKG, "build", "liblcv_hostsim_ops.so")
+    if not os.path.exists(ops):
+        import subprocess
+        subprocess.check_call(["make", "-s", "hostsim"], cwd=H.PKG)
+    import opcount
+    c = opcount.count(2)
+    per = c["per_update"]
+    for st in ("h2c_sswu", "hash_to_g2", "sig_decode", "g2_subgroup", "g1_aggregate", "miller_loop", "final_exp"):
+        assert per.get(st, {}).get("fp_mul", 0) > 0, st
+    for st in ("pre_checks", "nsc_htr"):
+        assert per[st]["sha"] > 0
+    # the programs' MUL counts are what the op counter sees (one per MUL op, not per lane)
+    # (+2 per inversion: the binary GCD's conversions out of / into Montgomery form)
+    import gen_programs as G
+
+    def muls(p):
+        ops = [v for r in p.rounds for v in r]
+        return sum(v.kind == "mul" for v in ops) + 2 * sum(v.kind == "inv" for v in ops)
+    assert per["final_exp"]["fp_mul"] == muls(G.make_fexp(16))
+    assert per["miller_loop"]["fp_mul"] == muls(G.make_miller(32))
+    tot = c["total_per_update"]
+    assert abs(sum(d["fp_mul"] for d in per.values()) - tot["fp_mul"]) < 1e-6
+
+
+def test_windowed_pow_hostsim(sim_verifier):
+    rng = np.random.default_rng(5)
+    xs = [0, 1, 2, P - 1, P - 2, (P - 1) // 2] + [int.from_bytes(rng.bytes(48), "big") % P for _ in range(20)]
+    xs += [x * x % P for x in xs[6:12]]
+    out = sim_verifier.debug_fp_pow(np.frombuffer(b"".join(x.to_bytes(48, "big") for x in xs), np.uint8))
+    for i, x in enumerate(xs):
+        b = out[i].tobytes()
+        assert int.from_bytes(b[:48], "big") == pow(x, (P + 1) // 4, P)
+        assert int.from_bytes(b[48:], "big") == pow(x, (P - 3) // 4, P)

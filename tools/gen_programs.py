@@ -968,6 +968,7 @@ def emit(progs, path):
         lines.append(f"#define LCV_PROG_{N}_SLOTS {p.nslots}")
         lines.append(f"#define LCV_PROG_{N}_NCONST {len(p.consts)}")
         lines.append(f"#define LCV_PROG_{N}_MAXSUM {p.max_abs_sum()}")
+        lines.append(f"#define LCV_PROG_{N}_ZERO {p.zero.slot}")
         for nm, s in sorted(p.state_slots.items(), key=lambda kv: kv[1]):
             lines.append(f"#define LCV_PROG_{N}_SLOT_{nm.upper()} {s}")
         lines.append(f"static const uint32_t kProg_{p.name}_hdr[{len(hdr)}] = {{")

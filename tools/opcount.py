@@ -21,15 +21,14 @@ from lcv._native import Lib  # noqa: E402
 from lcv.device import Verifier  # noqa: E402
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=8)
-    ap.add_argument("--participation", default="full")
-    args = ap.parse_args()
+def count(n: int = 8, participation: str = "full", npool: int = 1) -> dict:
+    """Per-stage algorithmic operation counts per update (one mark per kernel, so every operation
+    lands in exactly one stage).  Team programs count one Fp multiplication per MUL op of the
+    program (not per lane of a round) and (terms - 1) additions per combination."""
     lib = Lib(os.path.join(PKG, "build", "liblcv_hostsim_ops.so"))
     lib.dll.lcv_debug_opcounts.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
     v = Verifier(lib=lib)
-    sb = synth.generate(v, args.n, seed=2, participation=args.participation)
+    sb = synth.generate(v, n, seed=2, participation=participation, npool=npool)
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     ok, _ = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
     assert ok.all()
@@ -40,13 +39,23 @@ def main():
     for s, name in enumerate(names):
         fm, fa, sh = buf[3 * s], buf[3 * s + 1], buf[3 * s + 2]
         if fm or fa or sh:
-            per[name] = {"fp_mul": fm / args.n, "fp_add": fa / args.n, "sha": sh / args.n}
+            per[name] = {"fp_mul": fm / n, "fp_add": fa / n, "sha": sh / n,
+                         "int32_ops": (600 * fm + 24 * fa + 2100 * sh) / n}
     tot = {k: sum(d[k] for d in per.values()) for k in ("fp_mul", "fp_add", "sha")}
-    out = {"config": f"{args.n} synthetic Deneb updates, {args.participation} participation, all branches "
-                     f"(nsc pool of 1: HTR(next_sync_committee) amortised over the batch)",
-           "op_model": "INT32 ops = 600*fp_mul + 24*fp_add + 2100*sha (SURVEY.md 8(d))",
-           "per_update": per, "total_per_update": tot,
-           "int32_ops_per_update": 600 * tot["fp_mul"] + 24 * tot["fp_add"] + 2100 * tot["sha"]}
+    pool = "nsc pool of 1: HTR(next_sync_committee) amortised over the batch" if npool == 1 else \
+        f"{npool} distinct next_sync_committee values"
+    return {"config": f"{n} synthetic Deneb updates, {participation} participation, all branches ({pool})",
+            "op_model": "INT32 ops = 600*fp_mul + 24*fp_add + 2100*sha (SURVEY.md 8(d))",
+            "per_update": per, "total_per_update": tot,
+            "int32_ops_per_update": 600 * tot["fp_mul"] + 24 * tot["fp_add"] + 2100 * tot["sha"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--participation", default="full")
+    args = ap.parse_args()
+    out = count(args.n, args.participation)
     path = os.path.join(ROOT, "profiles", "opcounts.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
