@@ -153,6 +153,49 @@ LCV_FN void fp_mul_ps(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]
   fp_reduce_once(r, t);
 }
 #define LCV_MUL_IMPL fp_mul_ps
+#elif defined(LCV_CPU_FAST)
+// CPU-baseline build only (liblcv_cpu.so, bench.py's cpu_baseline leg): the same Montgomery product
+// (R = 2^384, identical representation and results) on 6 x 64-bit limbs with 128-bit products, the
+// natural x86-64 shape; the device and the test host simulation keep the 12 x 32-bit code above.
+static inline void fp_mul_cpu64(uint32_t r[12], const uint32_t a32[12], const uint32_t b32[12]) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint64_t a[6], b[6], p[6];
+  for (int k = 0; k < 6; ++k) {
+    a[k] = (uint64_t)a32[2 * k] | ((uint64_t)a32[2 * k + 1] << 32);
+    b[k] = (uint64_t)b32[2 * k] | ((uint64_t)b32[2 * k + 1] << 32);
+    p[k] = (uint64_t)PL[2 * k] | ((uint64_t)PL[2 * k + 1] << 32);
+  }
+  uint64_t inv = 1;
+  for (int k = 0; k < 6; ++k) inv *= 2 - p[0] * inv;  // p^-1 mod 2^64 (Newton)
+  const uint64_t n0 = 0 - inv;
+  uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 6; ++i) {
+    unsigned __int128 c = 0;
+    for (int j = 0; j < 6; ++j) {
+      c += (unsigned __int128)a[j] * b[i] + t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[6];
+    t[6] = (uint64_t)c;
+    t[7] = (uint64_t)(c >> 64);
+    const uint64_t m = t[0] * n0;
+    c = (unsigned __int128)m * p[0] + t[0];
+    c >>= 64;
+    for (int j = 1; j < 6; ++j) {
+      c += (unsigned __int128)m * p[j] + t[j];
+      t[j - 1] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[6];
+    t[5] = (uint64_t)c;
+    t[6] = t[7] + (uint64_t)(c >> 64);
+  }
+  uint32_t t32[12];
+  for (int k = 0; k < 6; ++k) { t32[2 * k] = (uint32_t)t[k]; t32[2 * k + 1] = (uint32_t)(t[k] >> 32); }
+  fp_reduce_once(r, t32);
+}
+#define LCV_MUL_IMPL fp_mul_cpu64
 #else
 #define LCV_MUL_IMPL fp_mul_impl
 #endif

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 counter passes of tools/pmc_collect.sh into one JSON per kernel (average per
+launch over the profiled launches), with the derived quantities bench.py's roofline block carries:
+
+  hbm_bytes_per_launch   = 2 * FETCH_SIZE + WRITE_SIZE (KB -> B; FETCH_SIZE doubled on gfx950, see
+                           MI355X_MICROARCH.md "FETCH_SIZE reports exactly 1/2 ...")
+  valu_busy              = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES  (fraction of a resident wave's cycles
+                           spent issuing VALU)
+  issue_busy             = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
+  mean_waves_per_simd    = SQ_WAVE_CYCLES / SQ_BUSY_CYCLES / 4  (SIMDs per CU; a ratio of counters on the
+                           same clock, independent of the duration measurement)
+  lds_bank_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE  (extra cycles per LDS-array cycle)
+  valu_insts_per_wave    = SQ_INSTS_VALU / SQ_WAVES
+
+    python tools/pmc_summary.py gpurun_out/pmc profiles/r02_vN/pmc.json [profiles/pmc_latest.json]
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+
+def short(name: str) -> str:
+    m = re.match(r"void (k_\w+<\w+>)", name)
+    return m.group(1) if m else name.split("(")[0][:60]
+
+
+def load(src: str):
+    acc = {}
+    for sub in sorted(os.listdir(src)):
+        d = os.path.join(src, sub)
+        if not os.path.isdir(d):
+            continue
+        for root, _, files in os.walk(d):
+            for f in files:
+                if not f.endswith("counter_collection.csv"):
+                    continue
+                for row in csv.DictReader(open(os.path.join(root, f))):
+                    k = short(row["Kernel_Name"])
+                    c = row["Counter_Name"]
+                    key = (row.get("Dispatch_Id") or row.get("Correlation_Id") or "")
+                    e = acc.setdefault(k, {}).setdefault(c, {})
+                    e[(sub, key)] = e.get((sub, key), 0.0) + float(row["Counter_Value"])
+    out = {}
+    for k, cs in acc.items():
+        out[k] = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+    return out
+
+
+def derive(c: dict) -> dict:
+    d = {"raw": {k: round(v, 1) for k, v in sorted(c.items())}}
+    g = c.get
+    if g("FETCH_SIZE") is not None and g("WRITE_SIZE") is not None:
+        d["hbm_bytes_per_launch"] = round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024)
+    if g("SQ_WAVE_CYCLES"):
+        if g("SQ_ACTIVE_INST_VALU") is not None:
+            d["valu_busy"] = round(g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES"), 4)
+        if g("SQ_ACTIVE_INST_ANY") is not None:
+            d["issue_busy"] = round(g("SQ_ACTIVE_INST_ANY") / g("SQ_WAVE_CYCLES"), 4)
+        if g("SQ_BUSY_CYCLES"):
+            d["mean_waves_per_simd"] = round(g("SQ_WAVE_CYCLES") / g("SQ_BUSY_CYCLES") / 4, 3)
+    if g("SQ_LDS_IDX_ACTIVE") and g("SQ_LDS_BANK_CONFLICT") is not None:
+        d["lds_bank_conflict_rate"] = round(g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE"), 4)
+    if g("SQ_WAVES") and g("SQ_INSTS_VALU") is not None:
+        d["valu_insts_per_wave"] = round(g("SQ_INSTS_VALU") / g("SQ_WAVES"), 1)
+    return d
+
+
+def main(src, dst, latest=None):
+    ks = {k: derive(c) for k, c in load(src).items()}
+    doc = {"source": src, "tool": "tools/pmc_collect.sh (rocprofv3 --kernel-trace --pmc, one pass per group)",
+           "kernels": ks}
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    json.dump(doc, open(dst, "w"), indent=1)
+    if latest:
+        json.dump(doc, open(latest, "w"), indent=1)
+    for k, d in ks.items():
+        if k.startswith("k_eng") or k in ("k_items<F_h2c_map>", "k_items<F_sig>"):
+            print(k, {x: d.get(x) for x in ("hbm_bytes_per_launch", "valu_busy", "issue_busy",
+                                              "mean_waves_per_simd", "lds_bank_conflict_rate", "valu_insts_per_wave")})
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
