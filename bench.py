@@ -94,17 +94,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
-    from lcv import synth
+    from lcv import multi, synth
     from lcv.device import Verifier
 
     v = Verifier(local)
+    # N > 1: one process per GPU, RCCL (over xGMI) inside liblcv.so for the verdict all-gather, the
+    # barrier and the max-over-ranks of the timed region; no PyTorch anywhere on the path
+    comm = multi.Comm(v, world, rank) if world > 1 else None
     t0 = time.perf_counter()
     sb = synth.generate(v, args.n, seed=2 + rank, participation=args.participation)
     log(f"[rank {rank}] generated {args.n} updates in {time.perf_counter() - t0:.1f}s")
@@ -115,35 +111,27 @@ def main():
     verdict = np.zeros(args.n, np.uint8)
     reason = np.zeros(args.n, np.uint8)
 
-    if dist is not None:
-        import torch
-        vdev = torch.zeros(args.n, dtype=torch.uint8, device=f"cuda:{local}")
-        gathered = torch.zeros(world * args.n, dtype=torch.uint8, device=f"cuda:{local}")
+    gathered = np.zeros(world * args.n, np.uint8)
 
-    def step():
-        if dist is None:
+    def step():  # every lcv call returns after its stream work is complete (device synchronised)
+        if comm is None:
             v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
         else:
-            v.validate_resident_dev(rb, sb.current_slot, sb.genesis_validators_root, vdev.data_ptr())
-            dist.all_gather_into_tensor(gathered, vdev)
+            comm.validate_sharded(rb, sb.current_slot, sb.genesis_validators_root, args.n, gathered)
 
     def sync():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        if comm is not None:
+            comm.barrier()
 
     for _ in range(args.warmup):
         step()
     # correctness of what is timed: every synthetic update is valid
-    if dist is None:
+    if comm is None:
         v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
         ok_all = bool((verdict == 1).all())
     else:
         step()
-        import torch
-        torch.cuda.synchronize()
-        ok_all = bool((gathered == 1).all().item())
+        ok_all = bool((gathered == 1).all())
     serial = pipe == (1, 1)
     stage_ms = {k: 0.0 for k in v.last_timings()}
     sync()
@@ -155,11 +143,8 @@ def main():
                 stage_ms[k] += ms
     sync()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    if comm is not None:
+        dt = comm.allreduce_max(dt)
 
     serial_ms, serial_ok = 1000 * dt / args.steps, ok_all
     if not serial:
@@ -181,9 +166,8 @@ def main():
     pcie_rate = args.n / (time.perf_counter() - t1)
 
     if rank != 0:
-        if dist is not None:
-            dist.barrier()
-            dist.destroy_process_group()
+        if comm is not None:
+            comm.close()
         return
     wire_out = wire_path(v, sb, args.n)
     total = world * args.n * args.steps
@@ -231,9 +215,8 @@ def main():
         except Exception as e:  # reported, never fatal to the GPU measurement
             out["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
 
 
 def wire_path(v, sb, n: int) -> dict:

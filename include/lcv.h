@@ -120,6 +120,20 @@ int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
 int lcv_last_timings(lcv_ctx* ctx, float* ms_out, int max_stages, int* nstages);
 const char* lcv_stage_name(int stage);
 
+/* ---- multi-GPU: one process and one context per GPU, updates sharded by contiguous
+ * index range, RCCL over xGMI for the one collective (the per-update verdict all-gather).  No reference
+ * counterpart: the reference is single-process (p2p-interface.md:69,99 is the ingress producing batches).
+ * lcv_comm_unique_id: rank 0 makes the 128-byte id (ncclGetUniqueId) and hands it to every rank. */
+int lcv_comm_unique_id(uint8_t* id128);
+int lcv_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id128);
+int lcv_comm_destroy(lcv_ctx* ctx);
+/* validate this rank's resident shard (n <= per_rank), all-gather every rank's per_rank verdict bytes
+ * (zero padded) into verdict_all_out (nranks * per_rank bytes, rank-major) */
+int lcv_validate_sharded(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot, const uint8_t* genesis_validators_root,
+                         uint64_t per_rank, uint8_t* verdict_all_out);
+/* max over ranks of one double (in place); doubles as a barrier */
+int lcv_comm_allreduce_max(lcv_ctx* ctx, double* inout);
+
 /* ---- bls.FastAggregateVerify (sync-protocol.md:464); py_ecc semantics (every key KeyValidated).
  * Any number of pubkeys (npk = 0 -> False), a message of any length (the light-client call site passes
  * a 32-byte signing root; other lengths take the device's byte-streamed expand_message_xmd). */

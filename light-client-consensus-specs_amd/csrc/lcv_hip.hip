@@ -4,6 +4,8 @@
 // lcv_last_timings() (and cross-checked with rocprofv3).  The kernels themselves live in the
 // lcv_k_*.hip units (one heavy stage per unit so they compile in parallel).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
 
 #include <new>
 #include <string>
@@ -25,6 +27,8 @@ struct Backend {
   int open_stage[BE_STREAMS] = {-1, -1, -1, -1};
   hipEvent_t open_ev[BE_STREAMS] = {};
   hipEvent_t fork_ev[BE_STREAMS] = {}, join_ev[BE_STREAMS] = {};
+  ncclComm_t comm = nullptr;  // RCCL communicator (lcv_comm_init), collectives on st[0]
+  double* comm_scalar = nullptr;
 };
 
 static int be_init(lcv_ctx* ctx, int device);
@@ -48,6 +52,11 @@ static void be_stage_begin(lcv_ctx* ctx, int stage);
 static void be_stage_end(lcv_ctx* ctx, int stage);
 static void be_reset_timings(lcv_ctx* ctx);
 static void be_collect_timings(lcv_ctx* ctx);
+static int be_comm_unique_id(uint8_t* id);
+static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id);
+static void be_comm_destroy(lcv_ctx* ctx);
+static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank);
+static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout);
 
 #include "lcv_driver.inc"
 #include "lcv_launch.hpp"
@@ -196,6 +205,51 @@ static void be_collect_timings(lcv_ctx* ctx) {
   }
   ctx->be.marks.clear();
   ctx->be.used = 0;
+}
+
+// ---- RCCL (over xGMI between the GPUs of one node): the verdict all-gather of lcv_validate_sharded
+static int nccl_fail(lcv_ctx* ctx, ncclResult_t r, const char* what) {
+  return fail(ctx, LCV_EDEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+}
+static int be_comm_unique_id(uint8_t* id) {
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return LCV_EDEVICE;
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return LCV_OK;
+}
+static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id) {
+  HIPCHK(ctx, hipSetDevice(ctx->be.device));
+  ncclUniqueId u;
+  memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  ncclResult_t r = ncclCommInitRank(&ctx->be.comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    ctx->be.comm = nullptr;
+    return nccl_fail(ctx, r, "ncclCommInitRank");
+  }
+  HIPCHK(ctx, hipMalloc((void**)&ctx->be.comm_scalar, sizeof(double)));
+  return LCV_OK;
+}
+static void be_comm_destroy(lcv_ctx* ctx) {
+  (void)hipSetDevice(ctx->be.device);
+  if (ctx->be.comm) (void)ncclCommDestroy(ctx->be.comm);
+  if (ctx->be.comm_scalar) (void)hipFree(ctx->be.comm_scalar);
+  ctx->be.comm = nullptr;
+  ctx->be.comm_scalar = nullptr;
+}
+static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank) {
+  HIPCHK(ctx, hipSetDevice(ctx->be.device));
+  ncclResult_t r = ncclAllGather(send, recv, per_rank, ncclUint8, ctx->be.comm, ctx->be.st[0]);
+  return r == ncclSuccess ? LCV_OK : nccl_fail(ctx, r, "ncclAllGather");
+}
+static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
+  HIPCHK(ctx, hipSetDevice(ctx->be.device));
+  hipStream_t s = ctx->be.st[0];
+  HIPCHK(ctx, hipMemcpyAsync(ctx->be.comm_scalar, inout, sizeof(double), hipMemcpyHostToDevice, s));
+  ncclResult_t r = ncclAllReduce(ctx->be.comm_scalar, ctx->be.comm_scalar, 1, ncclFloat64, ncclMax, ctx->be.comm, s);
+  if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllReduce");
+  HIPCHK(ctx, hipMemcpyAsync(inout, ctx->be.comm_scalar, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipStreamSynchronize(s));
+  return LCV_OK;
 }
 
 extern "C" int lcv_device_count(int* out) {

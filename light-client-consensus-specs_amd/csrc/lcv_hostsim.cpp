@@ -5,7 +5,10 @@
 #define LCV_HOSTSIM 1
 #include <atomic>
 #include <chrono>
+#include <fstream>
 #include <new>
+#include <thread>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string>
 #include <vector>
@@ -26,6 +29,11 @@ struct Backend {
   std::chrono::steady_clock::time_point t0[4];
   unsigned long long ops0[4][3] = {};
   unsigned long long ops[16][3] = {};
+  // test-only stand-in for the RCCL communicator: collectives through files in a directory shared by
+  // the ranks (the "unique id" is its path), so the multi-process path runs on the CPU (tests/test_multi.py)
+  std::string comm_dir;
+  int comm_rank = 0, comm_n = 1;
+  unsigned long long comm_round = 0;
 };
 
 static int be_init(lcv_ctx* ctx, int device);
@@ -49,6 +57,11 @@ static void be_stage_begin(lcv_ctx* ctx, int stage);
 static void be_stage_end(lcv_ctx* ctx, int stage);
 static void be_reset_timings(lcv_ctx* ctx);
 static void be_collect_timings(lcv_ctx* ctx);
+static int be_comm_unique_id(uint8_t* id);
+static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id);
+static void be_comm_destroy(lcv_ctx* ctx);
+static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank);
+static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout);
 
 #include "lcv_driver.inc"
 
@@ -109,6 +122,56 @@ static void be_reset_timings(lcv_ctx* ctx) {
   for (int s = 0; s < 16; ++s) for (int k = 0; k < 3; ++k) ctx->be.ops[s][k] = 0;
 }
 static void be_collect_timings(lcv_ctx*) {}
+
+static int be_comm_unique_id(uint8_t* id) {
+  char tmpl[] = "/tmp/lcv_comm_XXXXXX";
+  if (!mkdtemp(tmpl)) return LCV_EDEVICE;
+  memset(id, 0, 128);
+  memcpy(id, tmpl, strlen(tmpl));
+  return LCV_OK;
+}
+static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id) {
+  ctx->be.comm_dir.assign((const char*)id, strnlen((const char*)id, 128));
+  ctx->be.comm_rank = rank;
+  ctx->be.comm_n = nranks;
+  ctx->be.comm_round = 0;
+  return LCV_OK;
+}
+static void be_comm_destroy(lcv_ctx* ctx) { ctx->be.comm_dir.clear(); }
+// every rank writes <dir>/<round>.<rank> (atomically: temp file + rename), then reads all of them
+static int comm_exchange(lcv_ctx* ctx, const void* mine, size_t bytes, uint8_t* all) {
+  Backend& b = ctx->be;
+  const unsigned long long r = b.comm_round++;
+  auto name = [&](int k) { return b.comm_dir + "/" + std::to_string(r) + "." + std::to_string(k); };
+  {
+    const std::string tmp = name(b.comm_rank) + ".tmp";
+    std::ofstream f(tmp, std::ios::binary);
+    f.write((const char*)mine, (std::streamsize)bytes);
+    f.close();
+    if (!f || rename(tmp.c_str(), name(b.comm_rank).c_str()) != 0) return fail(ctx, LCV_EDEVICE, "hostsim comm: write");
+  }
+  for (int k = 0; k < b.comm_n; ++k) {
+    for (int t = 0;; ++t) {
+      std::ifstream f(name(k), std::ios::binary);
+      if (f) {
+        f.read((char*)all + (size_t)k * bytes, (std::streamsize)bytes);
+        if ((size_t)f.gcount() == bytes) break;
+      }
+      if (t > 120000) return fail(ctx, LCV_EDEVICE, "hostsim comm: timed out waiting for a rank");
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  }
+  return LCV_OK;
+}
+static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank) {
+  return comm_exchange(ctx, send, per_rank, recv);
+}
+static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
+  std::vector<double> all((size_t)ctx->be.comm_n);
+  LCV_TRY(comm_exchange(ctx, inout, sizeof(double), (uint8_t*)all.data()));
+  for (double x : all) *inout = x > *inout ? x : *inout;
+  return LCV_OK;
+}
 
 extern "C" int lcv_device_count(int* out) {
   if (!out) return LCV_EINVAL;

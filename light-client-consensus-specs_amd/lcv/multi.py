@@ -1,15 +1,26 @@
-"""Multi-GPU sharding of a batch of updates (one process per GPU, torch.distributed).
+"""Multi-GPU sharding of a batch of updates: one process and one liblcv context per GPU, no PyTorch.
 
 Updates are independent given one store snapshot, so a batch is split into
 contiguous index ranges, one per rank; each rank validates its shard on its own GPU and the only
-collective is one all-gather of the per-update verdict bytes (RCCL over xGMI with the "nccl"
-backend and device buffers; gloo with host buffers for the CPU tests).  No data-path exchange.
+collective is one all-gather of the per-update verdict bytes — RCCL over xGMI, device buffer to
+device buffer, inside liblcv.so (`lcv_validate_sharded`).  No data-path exchange.
+
+Rendezvous: rank 0 creates the 128-byte RCCL unique id (`lcv_comm_unique_id`) and publishes it in a
+file that the other ranks of the same launch (same parent process, same MASTER_PORT: all on one node)
+poll for.  The test suite runs the same code on the host simulation, whose stand-in collective
+exchanges files (tests/test_multi.py).
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
+import tempfile
+import time
 from typing import Optional, Tuple
 
 import numpy as np
+
+from ._native import LcvError, as_u8, ptr
 
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -19,27 +30,99 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def gather_verdicts(local: np.ndarray, n_total: int, world: int, device: Optional[str] = None) -> np.ndarray:
-    """All-gather the per-rank verdict bytes (shards from shard_bounds) into the full verdict array."""
-    import torch
-    import torch.distributed as dist
-    per = -(-n_total // world)  # padded shard length (all_gather needs equal sizes)
-    buf = torch.zeros(per, dtype=torch.uint8, device=device) if device else torch.zeros(per, dtype=torch.uint8)
-    buf[:len(local)] = torch.from_numpy(np.ascontiguousarray(local, np.uint8)).to(buf.device)
-    out = torch.zeros(world * per, dtype=torch.uint8, device=buf.device)
-    dist.all_gather_into_tensor(out, buf) if device else dist.all_gather(list(out.split(per)), buf)
-    full = out.cpu().numpy().reshape(world, per)
-    parts = [full[r, :shard_bounds(n_total, world, r)[1] - shard_bounds(n_total, world, r)[0]] for r in range(world)]
-    return np.concatenate(parts)
+def _id_path(key: Optional[str]) -> str:
+    if key is None:
+        key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    d = os.environ.get("LCV_RENDEZVOUS_DIR", tempfile.gettempdir())
+    return os.path.join(d, f"lcv_rccl_id_{key}")
 
 
-def validate_sharded(verifier, batch, current_slot: int, genesis_validators_root: bytes, world: int, rank: int,
-                     device: Optional[str] = None) -> np.ndarray:
+def rendezvous(lib, rank: int, world: int, key: Optional[str] = None, timeout: float = 300.0) -> bytes:
+    """The communicator id, made by rank 0 and read by every other rank of this launch."""
+    path = _id_path(key)
+    if rank == 0:
+        uid = np.zeros(128, np.uint8)
+        rc = lib.lcv_comm_unique_id(ptr(uid))
+        if rc != 0:
+            raise LcvError(f"lcv_comm_unique_id failed with status {rc}")
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid.tobytes())
+        os.replace(tmp, path)  # atomic: readers see the whole id or nothing
+        return uid.tobytes()
+    t0 = time.monotonic()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                b = f.read()
+            if len(b) == 128:
+                return b
+        except FileNotFoundError:
+            pass
+        if time.monotonic() - t0 > timeout:
+            raise LcvError(f"rendezvous: no communicator id at {path} after {timeout:.0f} s")
+        time.sleep(0.01)
+
+
+class Comm:
+    """The RCCL communicator of one rank (on `verifier`'s device)."""
+
+    def __init__(self, verifier, world: int, rank: int, key: Optional[str] = None):
+        self.v, self.world, self.rank = verifier, int(world), int(rank)
+        self.key = key
+        uid = rendezvous(verifier.lib, self.rank, self.world, key)
+        self.v._check(self.v.lib.lcv_comm_init(self.v.ctx, self.world, self.rank, ptr(as_u8(uid))), "lcv_comm_init")
+
+    def validate_sharded(self, rb, current_slot: int, genesis_validators_root: bytes, per_rank: int,
+                         out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Validate this rank's resident shard (rb.n <= per_rank) and all-gather every rank's verdict
+        bytes: (world * per_rank,) uint8, rank-major, each slice zero padded."""
+        gvr = as_u8(bytes(genesis_validators_root))
+        buf = out if out is not None else np.zeros(self.world * per_rank, np.uint8)
+        self.v._check(self.v.lib.lcv_validate_sharded(self.v.ctx, rb.handle, int(current_slot), ptr(gvr),
+                                                      int(per_rank), ptr(buf)), "lcv_validate_sharded")
+        return buf
+
+    def allreduce_max(self, x: float) -> float:
+        d = C.c_double(float(x))
+        self.v._check(self.v.lib.lcv_comm_allreduce_max(self.v.ctx, C.byref(d)), "lcv_comm_allreduce_max")
+        return d.value
+
+    def barrier(self) -> None:
+        self.allreduce_max(0.0)
+
+    def close(self) -> None:
+        if self.v is not None:
+            self.barrier()
+            if self.rank == 0:
+                try:
+                    os.remove(_id_path(self.key))
+                except OSError:
+                    pass
+            self.v.lib.lcv_comm_destroy(self.v.ctx)
+            self.v = None
+
+
+def unshard(gathered: np.ndarray, n_total: int, world: int) -> np.ndarray:
+    """Rank-major padded slices -> the n_total verdicts in batch order."""
+    per = gathered.size // world
+    parts = [gathered[r * per:r * per + (shard_bounds(n_total, world, r)[1] - shard_bounds(n_total, world, r)[0])]
+             for r in range(world)]
+    return np.concatenate(parts) if parts else gathered[:0]
+
+
+def validate_sharded(verifier, batch, current_slot: int, genesis_validators_root: bytes, comm: Comm) -> np.ndarray:
     """This rank validates its shard of `batch` (the full PackedUpdates, identical on every rank);
-    returns the full verdict array on every rank.  The store must already be set on `verifier`."""
+    returns the full verdict array (bool) on every rank.  The store must already be set on `verifier`."""
+    world, rank = comm.world, comm.rank
     lo, hi = shard_bounds(batch.n, world, rank)
+    per = -(-batch.n // world)
     if hi > lo:
-        ok, _ = verifier.validate(batch.slice(lo, hi), current_slot, genesis_validators_root)
-    else:
-        ok = np.zeros(0, bool)
-    return gather_verdicts(ok.astype(np.uint8), batch.n, world, device).astype(bool)
+        rb = verifier.upload(batch.slice(lo, hi))
+    else:  # an empty shard still joins the collective (a one-row dummy batch, verdict overwritten)
+        rb = verifier.upload(batch.slice(0, 1))
+    try:
+        g = comm.validate_sharded(rb, current_slot, genesis_validators_root, max(per, 1))
+    finally:
+        rb.free()
+    return unshard(g, batch.n, world).astype(bool)

@@ -1,6 +1,8 @@
-"""N > 1 path on CPU: world_size-2 gloo processes shard one batch, validate their shards on the host
-simulation of the kernels, and all-gather the verdicts (lcv/multi.py, the same code bench.py's
-sharding follows on RCCL)."""
+"""N > 1 path on CPU: world_size-2 processes shard one batch, validate their shards on the host
+simulation of the kernels and all-gather the verdicts through lcv/multi.py's Comm — the same code and
+C ABI (lcv_comm_init, lcv_validate_sharded, lcv_comm_allreduce_max) bench.py runs over RCCL on the
+GPUs; the host simulation's stand-in collective exchanges files.  A gloo run (torch.distributed) of
+the same shards checks the gathered verdicts independently."""
 import os
 import socket
 
@@ -19,6 +21,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
+    import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -28,8 +31,20 @@ def _worker(rank, world, port, q):
         kinds = np.array([0, 2, 4, 1, 5, 0, 6])
         sb = synth.generate(v, len(kinds), seed=31, kinds=kinds)  # identical on every rank (seeded)
         v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
-        full = multi.validate_sharded(v, sb.updates, sb.current_slot, sb.genesis_validators_root, world, rank)
-        q.put((rank, full.tolist(), sb.expected_verdict.tolist()))
+        comm = multi.Comm(v, world, rank, key=f"test_{port}")
+        full = multi.validate_sharded(v, sb.updates, sb.current_slot, sb.genesis_validators_root, comm)
+        t = comm.allreduce_max(float(rank + 1))
+        # independent check: gloo all-gather of the same shards' verdicts
+        lo, hi = multi.shard_bounds(sb.updates.n, world, rank)
+        ok, _ = v.validate(sb.updates.slice(lo, hi), sb.current_slot, sb.genesis_validators_root)
+        per = -(-sb.updates.n // world)
+        buf = torch.zeros(per, dtype=torch.uint8)
+        buf[:hi - lo] = torch.from_numpy(ok.astype(np.uint8))
+        parts = [torch.zeros(per, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        gloo = multi.unshard(torch.cat(parts).numpy(), sb.updates.n, world).astype(bool)
+        comm.close()
+        q.put((rank, full.tolist(), gloo.tolist(), sb.expected_verdict.tolist(), t))
     finally:
         dist.destroy_process_group()
 
@@ -57,5 +72,6 @@ def test_two_rank_gloo():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for rank, full, exp in res:
-        assert full == exp
+    for rank, full, gloo, exp, t in res:
+        assert full == exp == gloo
+        assert t == 2.0
