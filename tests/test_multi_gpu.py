@@ -1,0 +1,31 @@
+"""The RCCL path of lcv/multi.py on the GPU with one rank (the box has one GPU; the driver's 8-GPU
+scaling run exercises more ranks): communicator init from a rendezvous id, sharded validate with the
+device-to-device verdict all-gather, the max all-reduce used for bench timing, and teardown."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_one_rank(gpu_verifier):
+    if os.environ.get("LCV_TEST_HOSTSIM") == "1":
+        pytest.skip("RCCL: product library only")
+    from lcv import multi, synth
+    kinds = np.array([0, 2, 4, 0, 1, 5, 0, 6, 3, 0])
+    sb = synth.generate(gpu_verifier, len(kinds), seed=51, kinds=kinds)
+    gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    comm = multi.Comm(gpu_verifier, 1, 0, key=f"gputest_{os.getpid()}")
+    try:
+        full = multi.validate_sharded(gpu_verifier, sb.updates, sb.current_slot, sb.genesis_validators_root, comm)
+        assert list(full) == list(sb.expected_verdict)
+        rb = gpu_verifier.upload(sb.updates)
+        try:
+            g = comm.validate_sharded(rb, sb.current_slot, sb.genesis_validators_root, 16)
+        finally:
+            rb.free()
+        assert list(g[:len(kinds)].astype(bool)) == list(sb.expected_verdict) and not g[len(kinds):].any()
+        assert comm.allreduce_max(3.5) == 3.5
+    finally:
+        comm.close()

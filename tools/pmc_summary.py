@@ -7,8 +7,9 @@ launch over the profiled launches), with the derived quantities bench.py's roofl
   valu_busy              = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES  (fraction of a resident wave's cycles
                            spent issuing VALU)
   issue_busy             = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
-  mean_waves_per_simd    = SQ_WAVE_CYCLES / SQ_BUSY_CYCLES / 4  (SIMDs per CU; a ratio of counters on the
-                           same clock, independent of the duration measurement)
+  mean_waves_per_simd    = 4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024)  (SQ_WAVE_CYCLES counts
+                           quad-cycles per resident wave, summed; GRBM_GUI_ACTIVE is summed over the 8 XCDs,
+                           so / 8 is the kernel's cycles; 1024 SIMDs) — the time-averaged occupancy
   lds_bank_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE  (extra cycles per LDS-array cycle)
   valu_insts_per_wave    = SQ_INSTS_VALU / SQ_WAVES
 
@@ -58,8 +59,8 @@ def derive(c: dict) -> dict:
             d["valu_busy"] = round(g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES"), 4)
         if g("SQ_ACTIVE_INST_ANY") is not None:
             d["issue_busy"] = round(g("SQ_ACTIVE_INST_ANY") / g("SQ_WAVE_CYCLES"), 4)
-        if g("SQ_BUSY_CYCLES"):
-            d["mean_waves_per_simd"] = round(g("SQ_WAVE_CYCLES") / g("SQ_BUSY_CYCLES") / 4, 3)
+        if g("GRBM_GUI_ACTIVE"):
+            d["mean_waves_per_simd"] = round(4 * g("SQ_WAVE_CYCLES") / (g("GRBM_GUI_ACTIVE") / 8 * 1024), 3)
     if g("SQ_LDS_IDX_ACTIVE") and g("SQ_LDS_BANK_CONFLICT") is not None:
         d["lds_bank_conflict_rate"] = round(g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE"), 4)
     if g("SQ_WAVES") and g("SQ_INSTS_VALU") is not None:
