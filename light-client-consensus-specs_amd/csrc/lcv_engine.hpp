@@ -179,10 +179,6 @@ LCV_FN void eng_round(const ProgView& P, uint32_t r, uint32_t lane, uint32_t tea
 
 namespace lcv {
 
-// fp2 coefficient g_i (of w^i) -> its fp2 slot in the SoA Fp12 layout of soa_st_fp12 (c0.c0, c0.c1,
-// c0.c2, c1.c0, c1.c1, c1.c2 = g0, g2, g4, g1, g3, g5)
-LCV_FN uint32_t fp12_soa_slot(uint32_t g) { return (g & 1u) ? 3u + (g >> 1) : (g >> 1); }
-
 // Miller loop of both pairings.  Prologue (lane k < 12 loads input k): Q1 = H(m), Q2 = signature,
 // P1 = aggregate pubkey, P2 = -G1; an identity Q_k becomes (Q_k = G2 generator, P_k = (0, 0)), whose
 // lines are Fp2 constants killed by the final exponentiation (e(P, O) = 1).  Epilogue: f -> W.f.

@@ -1,0 +1,154 @@
+// lcv_functors_sop.hpp — team functors of the SOP programs (lcv_sop.hpp, tools/gen_sop.py): the pairing
+// check of bls.FastAggregateVerify (reference call site sync-protocol.md:464) as three kernels:
+//   F_sop_lines  one team of LCV_SOP_LINES_TEAM lanes per (update, pairing): the T walk over |x|,
+//                streaming the 68 sparse lines (a, b, c) of that pairing to W.lines (HBM, L2-resident);
+//   F_sop_acc    one team of 12 lanes (one Fp coefficient each) per update: f <- f^2 l1 l2 per step,
+//                the lines side-loaded one round ahead; output conj(f) to W.f;
+//   F_sop_fexp   one team of 12 lanes per update: final exponentiation (result e^3) and "== 1".
+#pragma once
+#include "lcv_functors.hpp"
+#include "lcv_sop.hpp"
+#include "lcv_sop_programs.inc"
+
+enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
+
+struct F_sop_lines {
+  Work W; SopView P;
+  static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12,
+                            SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
+  // item t: update i = t >> 1, pairing k = t & 1 (k = 0: e(PK_agg, H(m)); k = 1: e(-G1, signature))
+  LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
+  LCV_HD uint32_t* io_out(uint32_t t) const {
+    return W.lines + (size_t)(t >> 1) * SOP_LINE_WORDS + (size_t)(t & 1u) * SOP_LINE_VALS * 12;
+  }
+  // T = (Qx, Qy, 1), Q affine; (-xP, yP).  An identity Q becomes (G2 generator, P = (0, 0)): constant
+  // lines, killed by the final exponentiation (e(P, O) = 1).
+  LCV_HD void prologue(uint32_t t, uint32_t lane, uint32_t* lds) const {
+    const uint32_t i = t >> 1, k = t & 1u;
+    const bool id = k == 0 ? W.qh_inf[i] != 0 : W.sig_status[i] != PT_OK;
+    for (uint32_t v = lane; v < 12; v += TEAM) {
+      fp x;
+      uint32_t slot;
+      if (v < 8) {  // qx0 qx1 qy0 qy1, then the same into tx0 tx1 ty0 ty1
+        const uint32_t c = v & 3u;
+        if (id) {
+          fp2 g;
+          if (c < 2) LCV_FP2_SET(g, LCV_G2X);
+          else LCV_FP2_SET(g, LCV_G2Y);
+          x = (c & 1u) ? g.c1 : g.c0;
+        } else {
+          soa_ld_fp(x, k == 0 ? W.qh : W.qs, W.cap, i, c);
+        }
+        constexpr uint32_t QS[4] = {LCV_SOP_LINES_SLOT_QX0, LCV_SOP_LINES_SLOT_QX1, LCV_SOP_LINES_SLOT_QY0,
+                                    LCV_SOP_LINES_SLOT_QY1};
+        constexpr uint32_t TS[4] = {LCV_SOP_LINES_SLOT_TX0, LCV_SOP_LINES_SLOT_TX1, LCV_SOP_LINES_SLOT_TY0,
+                                    LCV_SOP_LINES_SLOT_TY1};
+        slot = v < 4 ? QS[c] : TS[c];
+      } else if (v < 10) {  // tz = (1, 0)
+        if (v == 8) fp_one(x);
+        else fp_zero(x);
+        slot = v == 8 ? LCV_SOP_LINES_SLOT_TZ0 : LCV_SOP_LINES_SLOT_TZ1;
+      } else {  // nxP, yP
+        if (k == 0) {
+          soa_ld_fp(x, W.pk, W.cap, i, v - 10);
+          if (v == 10) fp_neg(x, x);
+        } else if (v == 10) {
+          LCV_FP_SET(x, LCV_G1X_INIT);
+          fp_neg(x, x);
+        } else {
+          LCV_FP_SET(x, LCV_G1NEGY_INIT);
+        }
+        if (id) fp_zero(x);
+        slot = v == 10 ? LCV_SOP_LINES_SLOT_NXP : LCV_SOP_LINES_SLOT_YP;
+      }
+      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * slot + j] = x.v[j];
+    }
+  }
+  LCV_HD void epilogue(uint32_t, uint32_t, const uint32_t*) const {}
+};
+
+struct F_sop_acc {
+  Work W; SopView P;
+  static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12,
+                            SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
+  static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
+  LCV_HD const uint32_t* io_in(uint32_t i) const { return W.lines + (size_t)i * SOP_LINE_WORDS; }
+  LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
+  LCV_HD void prologue(uint32_t, uint32_t lane, uint32_t* lds) const {  // f = 1
+    if (lane >= 12) return;
+    fp x;
+    if (lane == 0) fp_one(x);
+    else fp_zero(x);
+    LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * lane + j] = x.v[j];
+  }
+  LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {  // slot 2g + c -> W.f
+    if (lane >= 12) return;
+    fp x;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = lds[12 * lane + j];
+    soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), x);
+  }
+};
+
+struct F_sop_fexp {
+  Work W; SopView P;
+  static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12,
+                            SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
+  static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
+  static_assert(LCV_SOP_FEXP_SLOT_R5_1 == LCV_SOP_FEXP_SLOT_R0_0 + 11, "r in consecutive slots");
+  LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
+  LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
+  LCV_HD void prologue(uint32_t i, uint32_t lane, uint32_t* lds) const {
+    if (lane >= 12) return;
+    fp x;
+    soa_ld_fp(x, W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u));
+    LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * lane + j] = x.v[j];
+  }
+  // the pairing value (e^3) to W.f; "== 1" to W.pair_ok
+  LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {
+    if (lane >= 12) return;
+    const uint32_t* r = lds + 12 * LCV_SOP_FEXP_SLOT_R0_0;
+    fp x;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = r[12 * lane + j];
+    soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), x);
+    if (lane == 0) {
+      fp one;
+      fp_one(one);
+      bool ok = fp_eq(x, one);
+      for (uint32_t k = 1; k < 12; ++k) {
+        uint32_t z = 0;
+        for (int j = 0; j < 12; ++j) z |= r[12 * k + j];
+        ok = ok && z == 0;
+      }
+      W.pair_ok[i] = ok ? 1 : 0;
+    }
+  }
+};
+
+#ifdef LCV_KERNEL_UNIT
+// The SOP round loop: one wave per block, 64 / TEAM teams (items) per wave, lanes past the last team
+// idle.  The round header is wave-uniform (scalar loads); each lane reads its record from global
+// memory (L2-resident program).  Blocks are one wave, so the barrier between rounds is a wave barrier.
+template <class F>
+__global__ __launch_bounds__(64) void k_sop(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
+  __shared__ uint32_t lds[F::SHARED_WORDS + G * F::LDS_WORDS];
+  const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
+  const uint32_t item = blockIdx.x * G + team;
+  const bool active = team < G && item < n;
+  uint32_t* my = lds + F::SHARED_WORDS + (team < G ? team : 0) * F::LDS_WORDS;
+  for (uint32_t k = threadIdx.x; k < F::SHARED_WORDS; k += 64) lds[k] = f.P.consts[k];
+  if (active) f.prologue(item, lane, my);
+  __syncthreads();
+  const uint32_t* io_in = active ? f.io_in(item) : nullptr;
+  uint32_t* io_out = active ? f.io_out(item) : nullptr;
+  const uint32_t R = f.P.rounds, ns = f.P.nslots;
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
+    const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 1]);
+    const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
+    if (active) lcv::sop_exec(h0, f.P.rec + off + lane * words, my, my, lds, ns, io_in, io_out);
+    __syncthreads();
+  }
+  if (active) f.epilogue(item, lane, my);
+}
+#endif

@@ -47,6 +47,7 @@ static int be_memset(lcv_ctx* ctx, void* p, int v, size_t bytes);
 static int be_sync(lcv_ctx* ctx);
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
+template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
 static int be_fork(lcv_ctx*) { return 0; }
 static int be_join(lcv_ctx*) { return 0; }
 static void be_use_stream(lcv_ctx* ctx, int k);
@@ -98,6 +99,26 @@ template <class F> static int be_launch_team(lcv_ctx*, const F& f, uint32_t n) {
   return LCV_OK;
 }
 static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = (k > 0 && k < 4) ? k : 0; }
+// SOP team kernels: every lane of a round reads the item's LDS as it was when the round began (the
+// device's lockstep wave), so the rounds run lane by lane against a snapshot
+template <class F> static int be_launch_sop(lcv_ctx*, const F& f, uint32_t n) {
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    std::vector<uint32_t> lds(F::LDS_WORDS, 0u), snap(F::LDS_WORDS, 0u), cl(F::SHARED_WORDS + 1, 0u);
+    for (uint32_t k = 0; k < F::SHARED_WORDS; ++k) cl[k] = f.P.consts[k];
+    for (uint32_t lane = 0; lane < F::TEAM; ++lane) f.prologue((uint32_t)i, lane, lds.data());
+    const uint32_t* io_in = f.io_in((uint32_t)i);
+    uint32_t* io_out = f.io_out((uint32_t)i);
+    for (uint32_t r = 0; r < f.P.rounds; ++r) {
+      snap = lds;
+      for (uint32_t lane = 0; lane < F::TEAM; ++lane)
+        lcv::sop_round(f.P, r, lane, snap.data(), lds.data(), cl.data(), io_in, io_out);
+    }
+    for (uint32_t lane = 0; lane < F::TEAM; ++lane) f.epilogue((uint32_t)i, lane, lds.data());
+  }
+  return LCV_OK;
+}
+
 static void be_stage_begin(lcv_ctx* ctx, int stage) {
   Backend& b = ctx->be;
   b.open_stage[b.cur] = stage;

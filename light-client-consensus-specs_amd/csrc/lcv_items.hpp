@@ -76,8 +76,13 @@ struct Work {
   uint8_t* pair_ok;      // [cap]
   uint8_t* verdict;      // [cap]
   uint8_t* reason;       // [cap]
+  uint32_t* lines;       // [item][2 pairings][6 * 68 line values][12]  (SOP Miller loop: lines -> accumulation)
   uint32_t msg_b0;       // 1: W.msg already holds expand_message_xmd's b0 (arbitrary-length messages)
 };
+
+// fp2 coefficient g_i (of w^i) -> its fp2 slot in the SoA Fp12 layout of soa_st_fp12 (c0.c0, c0.c1,
+// c0.c2, c1.c0, c1.c1, c1.c2 = g0, g2, g4, g1, g3, g5)
+LCV_FN uint32_t fp12_soa_slot(uint32_t g) { return (g & 1u) ? 3u + (g >> 1) : (g >> 1); }
 
 // ---- SoA helpers
 LCV_FN void soa_ld_fp(fp& r, const uint32_t* base, size_t cap, size_t i, size_t slot) {

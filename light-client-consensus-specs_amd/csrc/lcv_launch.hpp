@@ -9,6 +9,7 @@
 
 template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t s);
 template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s);
+template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s);
 
 #ifdef LCV_KERNEL_UNIT
 template <class F>
@@ -49,6 +50,15 @@ template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStr
   else hipLaunchKernelGGL(k_team<F>, dim3(blocks), dim3(64), 0, s, f, n);
   return hipGetLastError();
 }
+// SOP functors (lcv_functors_sop.hpp): the k_sop round loop, 64 / TEAM items per one-wave block
+template <class F> __global__ void k_sop(F f, uint32_t n);
+template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s) {
+  constexpr uint32_t G = 64 / F::TEAM;
+  const uint32_t blocks = (n + G - 1) / G;
+  hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), 0, s, f, n);
+  return hipGetLastError();
+}
+#define LCV_INSTANTIATE_SOP(F) template hipError_t lcv_hip_launch_sop<F>(const F&, uint32_t, hipStream_t);
 #define LCV_INSTANTIATE(F) template hipError_t lcv_hip_launch<F>(const F&, uint32_t, hipStream_t);
 #define LCV_INSTANTIATE_TEAM(F) template hipError_t lcv_hip_launch_team<F>(const F&, uint32_t, hipStream_t);
 #endif

@@ -1,0 +1,812 @@
+#!/usr/bin/env python3
+"""Generate the SOP ("sum of products") team programs of liblcv.so (csrc/lcv_sop_programs.inc): the
+Miller loop (line precompute + accumulation) and the final exponentiation of the two-pairing check
+inside FastAggregateVerify (reference call site sync-protocol.md:464).
+
+Why a second engine (round-1's lcv_engine.hpp interprets one Fp multiplication per lane per round):
+on gfx950 a fully reduced Montgomery product costs 288 v_mad_u64_u32, and an interpreter that issues
+one product per lane per round spends more on operand evaluation, LIN lanes and round latency than on
+the product (profiles/r02_v1: VALU busy 0.42-0.50, 1.0-2.4 waves/SIMD).  Here every lane op is
+
+    dst = REDC( sum_k  m_k * X_k * Y_k  +  R * (c_0 v_a + c_1 v_b) )  mod p          (R = 2^384)
+
+with X_k, Y_k = (+-v) (+-v) operand pairs read from the team's LDS slots.  The K products accumulate
+unreduced in a 25-word double-width accumulator and ONE Montgomery reduction closes the op (lazy
+reduction): an Fp12 squaring is 12 lanes x 7 products in one round, a cyclotomic squaring 12 lanes x 3
+products in one round, a sparse line product 12 lanes x 6 products.  Lanes of a team are one Fp
+coefficient each (team 12 = one Fp12), five teams per wave.
+
+Programs are explicit lists of rounds written at the Fp-coefficient level from the tower formulas
+(Fp12 = Fp2[w]/(w^6 - xi), xi = 1 + u, coefficient order g0..g5 of w^i).  An op may write a slot that
+ops of the same round read (in place): the team lives in one wave, every LDS read of a round is issued
+before its single store, and LDS operations of one wave complete in order.
+
+The generator EMULATES every program with Python integers exactly as the device computes (Montgomery
+representatives, unreduced accumulator, REDC, the header's conditional-subtraction count) and checks
+accumulator and result bounds and the results against oracle/bls12_381.py.
+
+    python tools/gen_sop.py [--check] [--out path]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+X_ABS = 0xD201000000010000
+R = 1 << 384
+RINV = pow(R, -1, P)
+NP = (-pow(P, -1, R)) % R          # -p^-1 mod R (REDC)
+ACC_BITS = 800                     # 25 x 32-bit accumulator words
+MAXK = 15
+SLOT_MASK = 0xFFF
+NEG = 0x8000                       # term halfword: slot | NEG
+
+
+def mont(x):
+    return x * R % P
+
+
+def unmont(x):
+    return x * RINV % P
+
+
+# ============================================================================ program representation
+class T:
+    """An operand term: slot, negated?  (the device reads p - v for a negated term)."""
+    __slots__ = ("slot", "neg")
+
+    def __init__(self, slot, neg=False):
+        self.slot, self.neg = slot, neg
+
+    def __invert__(self):
+        return T(self.slot, not self.neg)
+
+    def __repr__(self):
+        return ("-" if self.neg else "") + f"s{self.slot}"
+
+
+class Op:
+    """dst = REDC(sum m*X*Y + R*sum c*v) (kind 'sop'), or dst = (add-in value)^-1 (kind 'inv')."""
+
+    def __init__(self, dst, prods=(), adds=(), kind="sop", load=None, emit=None):
+        self.dst = dst
+        # a negative multiplier is folded into X's term signs: m > 0 from here on
+        self.prods = [(list(x) if m > 0 else [~t for t in x], list(y), abs(int(m))) for x, y, m in prods]
+        self.adds = [(int(s), int(c)) for s, c in adds]
+        self.kind = kind
+        self.load = load    # (ld_slot, io index): side-load of an Fp value from the program's input stream
+        self.emit = emit    # io index: the result is also written to the program's output stream
+        for x, y, m in self.prods:
+            assert 1 <= len(x) <= 2 and 1 <= len(y) <= 2 and m != 0
+        assert len(self.adds) <= 2
+
+
+class Program:
+    def __init__(self, name, team):
+        self.name, self.team = name, team
+        self.rounds = []
+        self.consts = {}        # value (canonical) -> index
+        self.nslots = 0
+        self.named = {}         # name -> slot (inputs / outputs the kernel's prologue / epilogue use)
+        self.free = []
+
+    # slots
+    def alloc(self, name=None):
+        if self.free:
+            s = self.free.pop()
+        else:
+            s = self.nslots
+            self.nslots += 1
+        if name:
+            self.named[name] = s
+        return s
+
+    def alloc_n(self, n, name=None):
+        out = [self.alloc() for _ in range(n)]
+        if name:
+            for k, s in enumerate(out):
+                self.named[f"{name}{k}"] = s
+        return out
+
+    def release(self, slots):
+        self.free.extend(slots)
+
+    def const(self, v):
+        v %= P
+        if v not in self.consts:
+            self.consts[v] = len(self.consts)
+        return ("c", self.consts[v])
+
+    def round(self, ops):
+        ops = [o for o in ops if o is not None]
+        assert 1 <= len(ops) <= self.team, (self.name, len(ops))
+        dsts = [o.dst for o in ops] + [o.load[0] for o in ops if o.load]
+        assert len(dsts) == len(set(dsts)), "two ops of a round write one slot"
+        self.rounds.append(ops)
+
+    # ------------------------------------------------------------ finalise: slot numbers of constants
+    def finalize(self):
+        if 0 not in self.consts:
+            self.consts[0] = len(self.consts)
+        self.base_const = self.nslots
+        self.zero = self.base_const + self.consts[0]
+        assert self.base_const + len(self.consts) < SLOT_MASK
+
+    def sl(self, s):
+        if isinstance(s, tuple):
+            return self.base_const + s[1]
+        return s
+
+    def const_list(self):
+        out = [0] * len(self.consts)
+        for v, k in self.consts.items():
+            out[k] = v
+        return out
+
+    # ------------------------------------------------------------ bounds: conditional-subtraction steps
+    @staticmethod
+    def op_bounds(op):
+        """(T bound, REDC result bound) with every stored value < p and each term <= p."""
+        tmax = 0
+        for x, y, m in op.prods:
+            tmax += abs(m) * len(x) * P * len(y) * P
+        tmax += R * sum(abs(c) for _, c in op.adds) * P
+        return tmax, tmax // R + P
+
+    def red_steps(self, op):
+        tmax, res = self.op_bounds(op)
+        assert tmax < (1 << ACC_BITS), "accumulator overflow"
+        k = 0
+        while (P << k) <= res:
+            k += 1
+        return k
+
+    # ------------------------------------------------------------ encoding
+    def encode(self):
+        """hdr: 4 u32 per round (wave-uniform):
+             w0 = K | nadd << 4 | mflag << 6 | x2 << 7 | y2 << 8 | neg << 9 | inv << 10 | load << 11 |
+                  emit << 12 | red << 16 | used << 24
+             w1 = record offset (u32 words), w2 = record words per lane, w3 = 0
+           rec: per lane (T lanes per round; lanes >= used: dst = SLOT_NONE):
+             r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;  r1 = io index;
+             r2, r3 = add-in term: slot | coef << 16 (signed 16-bit);  then per product k:
+             [x0 | x1 << 16], [y0 | y1 << 16], [m]    (term = slot | NEG; padding = zero const)"""
+        self.finalize()
+        hdr, rec = [], []
+        z = self.zero
+        for ops in self.rounds:
+            K = max(len(o.prods) for o in ops)
+            assert K <= MAXK
+            nadd = max(len(o.adds) for o in ops)
+            mflag = any(abs(m) != 1 for o in ops for _, _, m in o.prods)
+            x2 = any(len(x) == 2 for o in ops for x, _, _ in o.prods)
+            y2 = any(len(y) == 2 for o in ops for _, y, _ in o.prods)
+            neg = any(t.neg for o in ops for x, y, _ in o.prods for t in x + y)
+            inv = any(o.kind == "inv" for o in ops)
+            load = any(o.load for o in ops)
+            emit = any(o.emit is not None for o in ops)
+            red = max(self.red_steps(o) for o in ops)
+            words = 4 + 3 * K
+            hdr += [K | nadd << 4 | int(mflag) << 6 | int(x2) << 7 | int(y2) << 8 | int(neg) << 9 | int(inv) << 10 |
+                    int(load) << 11 | int(emit) << 12 | red << 16 | len(ops) << 24, len(rec), words, 0]
+            for lane in range(self.team):
+                w = [0] * words
+                if lane >= len(ops):
+                    w[0] = SLOT_MASK
+                    w[2] = w[3] = z
+                    for k in range(K):
+                        w[4 + 3 * k:7 + 3 * k] = [z | z << 16, z | z << 16, 1]
+                    rec += w
+                    continue
+                o = ops[lane]
+                flags = (1 if o.kind == "inv" else 0) | (2 if o.load else 0) | (4 if o.emit is not None else 0)
+                w[0] = self.sl(o.dst) | flags << 12 | ((self.sl(o.load[0]) if o.load else 0) << 16)
+                w[1] = (o.load[1] if o.load else o.emit if o.emit is not None else 0)
+                assert not (o.load and o.emit is not None)
+                for j in range(2):
+                    if j < len(o.adds):
+                        s, c = o.adds[j]
+                        assert -32768 <= c <= 32767
+                        w[2 + j] = self.sl(s) | ((c & 0xFFFF) << 16)
+                    else:
+                        w[2 + j] = z
+                for k in range(K):
+                    if k < len(o.prods):
+                        x, y, m = o.prods[k]
+                        if m < 0:
+                            x, m = [~t for t in x], -m
+                        th = lambda t: self.sl(t.slot) | (NEG if t.neg else 0)  # noqa: E731
+                        xs = [th(t) for t in x] + [z] * (2 - len(x))
+                        ys = [th(t) for t in y] + [z] * (2 - len(y))
+                        w[4 + 3 * k:7 + 3 * k] = [xs[0] | xs[1] << 16, ys[0] | ys[1] << 16, m]
+                    else:
+                        w[4 + 3 * k:7 + 3 * k] = [z | z << 16, z | z << 16, 1]
+                rec += w
+        return hdr, rec
+
+    # ------------------------------------------------------------ emulation (device semantics)
+    def emulate(self, mem, io_in=None, io_out=None):
+        """mem: slot -> Montgomery representative (< p).  Executes the ENCODED program."""
+        hdr, rec = self.encode()
+        cl = self.const_list()
+        for k, v in enumerate(cl):
+            mem[self.base_const + k] = mont(v)
+        z = self.zero
+        for r in range(len(hdr) // 4):
+            w0, off, words = hdr[4 * r], hdr[4 * r + 1], hdr[4 * r + 2]
+            K, nadd, mflag, red, used = w0 & 15, (w0 >> 4) & 3, (w0 >> 6) & 1, (w0 >> 16) & 31, w0 >> 24
+            writes = []
+            for lane in range(self.team):
+                w = rec[off + lane * words:off + (lane + 1) * words]
+                dst = w[0] & SLOT_MASK
+                if lane >= used:
+                    assert dst == SLOT_MASK
+                    continue
+
+                def term(h):
+                    s = h & SLOT_MASK
+                    v = mem[s]
+                    assert 0 <= v < P
+                    return (P - v) if h & NEG else v
+                acc = 0
+                for k in range(K):
+                    a, b, m = w[4 + 3 * k:7 + 3 * k]
+                    X = term(a & 0xFFFF) + term(a >> 16)
+                    Y = term(b & 0xFFFF) + term(b >> 16)
+                    if mflag:
+                        X *= m
+                    else:
+                        assert m == 1
+                    assert X < (1 << 416) and Y < (1 << 384)
+                    acc += X * Y
+                for j in range(nadd):
+                    s, c = w[2 + j] & SLOT_MASK, w[2 + j] >> 16
+                    c = c - 65536 if c >= 32768 else c
+                    v = mem[s]
+                    acc += R * (abs(c) * ((P - v) if c < 0 else v))
+                assert acc < (1 << ACC_BITS)
+                m_ = (acc % R) * NP % R
+                res = (acc + m_ * P) // R
+                for s_ in range(red - 1, -1, -1):
+                    if res >= (P << s_):
+                        res -= P << s_
+                assert res < P, (self.name, r, lane)
+                flags = (w[0] >> 12) & 7
+                if flags & 1:  # inversion of the add-in value (its first term)
+                    res = mont(pow(unmont(res), P - 2, P)) if res else 0
+                if flags & 2:
+                    writes.append((w[0] >> 16, io_in[w[1]]))
+                if flags & 4:
+                    io_out[w[1]] = res
+                writes.append((dst, res))
+            for s, v in writes:
+                mem[s] = v
+        return mem
+
+    def stats(self):
+        ops = sum(len(r) for r in self.rounds)
+        prods = sum(len(o.prods) for r in self.rounds for o in r)
+        slots = sum(self.team * max(len(o.prods) for o in r) for r in self.rounds)
+        return (f"{self.name}: team {self.team}, {len(self.rounds)} rounds, {ops} ops, {prods} products "
+                f"(+{ops} REDC), {100.0 * prods / max(1, slots):.1f}% of product slots used, "
+                f"{self.nslots} LDS slots ({self.nslots * 48} B/item), {len(self.consts)} constants")
+
+
+# ============================================================================ formula helpers
+def fp2_prod(x, y, comp, xi=False, m=1):
+    """Products of component `comp` of (xi *) x*y for Fp2 views x = (x0, x1), y = (y0, y1)."""
+    x0, x1 = x
+    y0, y1 = y
+    if not xi:
+        return [([x0], [y0], m), ([~x1], [y1], m)] if comp == 0 else [([x0], [y1], m), ([x1], [y0], m)]
+    if comp == 0:   # x0 (y0 - y1) - x1 (y0 + y1)
+        return [([x0], [y0, ~y1], m), ([~x1], [y0, y1], m)]
+    return [([x0], [y0, y1], m), ([x1], [y0, ~y1], m)]
+
+
+def fp2_sqr(x, comp, xi=False, m=1):
+    """(xi *) x^2: x^2 = (x0 + x1)(x0 - x1) + 2 x0 x1 u."""
+    x0, x1 = x
+    base = ([x0, x1], [x0, ~x1], m)
+    if not xi:
+        return [base] if comp == 0 else [([x0], [x1], 2 * m)]
+    if comp == 0:
+        return [base, ([~x0], [x1], 2 * m)]
+    return [base, ([x0], [x1], 2 * m)]
+
+
+def neg2(x):
+    return (~x[0], ~x[1])
+
+
+def slots2(p, name=None):
+    a = p.alloc(name + "0" if name else None)
+    b = p.alloc(name + "1" if name else None)
+    return (T(a), T(b))
+
+
+def fp12_slots(p, name=None):
+    return [slots2(p, f"{name}{i}_" if name else None) for i in range(6)]
+
+
+def conj12(f):
+    return [g if i % 2 == 0 else neg2(g) for i, g in enumerate(f)]
+
+
+def dst_of(view):
+    assert not view.neg
+    return view.slot
+
+
+def fp12_sqr_ops(f, out):
+    """out = f^2 (schoolbook over Fp2, symmetric pairs): 12 ops, <= 7 products each."""
+    ops = []
+    for k in range(6):
+        for comp in range(2):
+            prods = []
+            for i in range(6):
+                for j in range(i, 6):
+                    s = i + j
+                    if s % 6 != k:
+                        continue
+                    xi = s >= 6
+                    if i == j:
+                        prods += fp2_sqr(f[i], comp, xi)
+                    else:
+                        prods += fp2_prod(f[i], f[j], comp, xi, 2)
+            ops.append(Op(dst_of(out[k][comp]), prods))
+    return ops
+
+
+def fp12_mul_ops(a, b, out):
+    """out = a*b (dense, schoolbook over Fp2): 12 ops, 12 products each."""
+    ops = []
+    for k in range(6):
+        for comp in range(2):
+            prods = []
+            for i in range(6):
+                j = (k - i) % 6
+                prods += fp2_prod(a[i], b[j], comp, xi=(i + j >= 6))
+            ops.append(Op(dst_of(out[k][comp]), prods))
+    return ops
+
+
+def fp12_mul_line_ops(f, line, out):
+    """out = f * (a + b w^2 + c w^3): 12 ops, 6 products each."""
+    a, b, c = line
+    ops = []
+    for k in range(6):
+        for comp in range(2):
+            prods = []
+            for j, l in ((0, a), (2, b), (3, c)):
+                i = (k - j) % 6
+                prods += fp2_prod(f[i], l, comp, xi=(i + j >= 6))
+            ops.append(Op(dst_of(out[k][comp]), prods))
+    return ops
+
+
+def cyclo_sqr_ops(g, out):
+    """Granger-Scott cyclotomic squaring, one round: z = [3A0 - 2g0, 3 xi C1 + 2g1, 3B0 - 2g2,
+    3A1 + 2g3, 3C0 - 2g4, 3B1 + 2g5] with (A0, A1) = (g0^2 + xi g3^2, 2 g0 g3), (B0, B1) from (g1, g4),
+    (C0, C1) from (g2, g5).  12 ops, <= 3 products + one add-in each."""
+    ops = []
+    pairs = {0: (0, 3), 2: (1, 4), 4: (2, 5)}   # output index -> (x0, x1) of its Fp4 square, "0" part
+    for k in range(6):
+        for comp in range(2):
+            add_c = 2 if k % 2 else -2
+            gk = g[k][comp]
+            adds = [(gk.slot, add_c if not gk.neg else -add_c)]
+            if k in (0, 2, 4):   # 3 (x0^2 + xi x1^2) - 2 g_k  with (x0, x1) = (g0, g3) | (g1, g4) | (g2, g5)
+                x0, x1 = pairs[k]
+                prods = fp2_sqr(g[x0], comp, False, 3) + fp2_sqr(g[x1], comp, True, 3)
+            elif k == 3:         # 3 * 2 g0 g3 + 2 g3
+                prods = fp2_prod(g[0], g[3], comp, False, 6)
+            elif k == 5:         # 3 * 2 g1 g4 + 2 g5
+                prods = fp2_prod(g[1], g[4], comp, False, 6)
+            else:                # k == 1: 3 xi (2 g2 g5) + 2 g1
+                prods = fp2_prod(g[2], g[5], comp, True, 6)
+            ops.append(Op(dst_of(out[k][comp]), prods, adds))
+    return ops
+
+
+def copy_ops(src, dst):
+    """dst = src (views may carry negations): add-in only ops."""
+    return [Op(dst_of(d), [], [(s.slot, -1 if s.neg else 1)]) for s, d in zip(src, dst)]
+
+
+def flat12(f):
+    return [t for g in f for t in g]
+
+
+# ============================================================================ Miller loop: lines
+def line_program(team=10):
+    """One pairing's T walk over |x| (63 doublings, 5 additions; the projective doubling of
+    gen_programs.line_dbl scaled by 4, no halvings), emitting per step the sparse line
+    (a, b, c) = (c00, c01 * (-xP), c11 * yP), 6 Fp values, io index 6 * step + j."""
+    p = Program("lines", team)
+    qx, qy = slots2(p, "qx"), slots2(p, "qy")
+    nxP, yP = T(p.alloc("nxp")), T(p.alloc("yp"))
+    X, Y, Z = slots2(p, "tx"), slots2(p, "ty"), slots2(p, "tz")
+    B, Cp, J, XY, YZ = (slots2(p) for _ in range(5))
+    BmF, BpF = slots2(p), slots2(p)
+    la, lb, lc = slots2(p), slots2(p), slots2(p)
+    th, lam, Cc, D, E, F, G, H, GmH = (slots2(p) for _ in range(9))
+    one = T(p.const(1))
+    step = 0
+
+    for bit in bin(X_ABS)[3:]:
+        # ---- doubling
+        p.round([Op(dst_of(B[c]), fp2_sqr(Y, c)) for c in range(2)] +
+                [Op(dst_of(Cp[c]), fp2_sqr(Z, c, xi=True)) for c in range(2)] +
+                [Op(dst_of(J[c]), fp2_sqr(X, c)) for c in range(2)] +
+                [Op(dst_of(XY[c]), fp2_prod(X, Y, c)) for c in range(2)] +
+                [Op(dst_of(YZ[c]), fp2_prod(Y, Z, c)) for c in range(2)])
+        # line: a = B - 12 C', b = 3 J * nxP, c = 2 YZ * yP ;  B -+ 3E with E = 12 C'
+        ops = [Op(dst_of(BmF[c]), [], [(B[c].slot, 1), (Cp[c].slot, -36)]) for c in range(2)]
+        ops += [Op(dst_of(BpF[c]), [], [(B[c].slot, 1), (Cp[c].slot, 36)]) for c in range(2)]
+        ops += [Op(dst_of(la[c]), [], [(B[c].slot, 1), (Cp[c].slot, -12)], emit=6 * step + c) for c in range(2)]
+        ops += [Op(dst_of(lb[c]), [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
+        ops += [Op(dst_of(lc[c]), [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
+        p.round(ops)
+        # T: X = 2 XY (B - 3E), Y = (B + 3E)^2 - 1728 C'^2, Z = 8 B YZ
+        ops = [Op(dst_of(X[c]), fp2_prod(XY, BmF, c, m=2)) for c in range(2)]
+        ops += [Op(dst_of(Y[c]), fp2_sqr(BpF, c) + fp2_sqr(Cp, c, m=-1728)) for c in range(2)]
+        ops += [Op(dst_of(Z[c]), fp2_prod(B, YZ, c, m=8)) for c in range(2)]
+        p.round(ops)
+        step += 1
+        if bit == "1":
+            # ---- addition T + Q: theta = Y - qy Z, lam = X - qx Z
+            ops = [Op(dst_of(th[c]), fp2_prod(qy, Z, c, m=-1), [(Y[c].slot, 1)]) for c in range(2)]
+            ops += [Op(dst_of(lam[c]), fp2_prod(qx, Z, c, m=-1), [(X[c].slot, 1)]) for c in range(2)]
+            p.round(ops)
+            # C = theta^2, D = lam^2; line (theta qx - lam qy, theta * nxP, lam * yP)
+            ops = [Op(dst_of(Cc[c]), fp2_sqr(th, c)) for c in range(2)]
+            ops += [Op(dst_of(D[c]), fp2_sqr(lam, c)) for c in range(2)]
+            ops += [Op(dst_of(la[c]), fp2_prod(th, qx, c) + fp2_prod(lam, qy, c, m=-1), emit=6 * step + c)
+                    for c in range(2)]
+            ops += [Op(dst_of(lb[c]), [([th[c]], [nxP], 1)], emit=6 * step + 2 + c) for c in range(2)]
+            ops += [Op(dst_of(lc[c]), [([lam[c]], [yP], 1)], emit=6 * step + 4 + c) for c in range(2)]
+            p.round(ops)
+            # E = lam D, F = Z C, G = X D
+            ops = [Op(dst_of(E[c]), fp2_prod(lam, D, c)) for c in range(2)]
+            ops += [Op(dst_of(F[c]), fp2_prod(Z, Cc, c)) for c in range(2)]
+            ops += [Op(dst_of(G[c]), fp2_prod(X, D, c)) for c in range(2)]
+            p.round(ops)
+            # H = E + F - 2G ; G - H = 3G - E - F   (third terms as products with the constant 1)
+            ops = [Op(dst_of(H[c]), [([G[c]], [one], -2)], [(E[c].slot, 1), (F[c].slot, 1)]) for c in range(2)]
+            ops += [Op(dst_of(GmH[c]), [([F[c]], [one], -1)], [(G[c].slot, 3), (E[c].slot, -1)]) for c in range(2)]
+            p.round(ops)
+            # X = lam H, Y = theta (G - H) - Y E, Z = Z E
+            ops = [Op(dst_of(X[c]), fp2_prod(lam, H, c)) for c in range(2)]
+            ops += [Op(dst_of(Y[c]), fp2_prod(th, GmH, c) + fp2_prod(Y, E, c, m=-1)) for c in range(2)]
+            ops += [Op(dst_of(Z[c]), fp2_prod(Z, E, c)) for c in range(2)]
+            p.round(ops)
+            step += 1
+    p.nsteps = step
+    return p
+
+
+def acc_program(team=12, nsteps=68):
+    """Accumulate f <- f^2 * L1(step) * L2(step) over the Miller steps (no squaring in the first and
+    in the addition steps, which follow their doubling step in the same loop iteration), then f^x = conj.
+    Lines stream in from the line programs' outputs: io index (6 * step + j) for pairing 1 and
+    (6 * nsteps + 6 * step + j) for pairing 2, side-loaded into L1/L2 slots one round ahead."""
+    p = Program("miller_acc", team)
+    f = fp12_slots(p, "f")
+    L = [[slots2(p) for _ in range(3)] for _ in range(2)]   # two lines: (a, b, c)
+    # step kinds in loop order (dbl, then add when the bit is 1)
+    kinds = []
+    for bit in bin(X_ABS)[3:]:
+        kinds.append("dbl")
+        if bit == "1":
+            kinds.append("add")
+    assert len(kinds) == nsteps
+
+    def loads(step):
+        ops = []
+        for k in range(2):
+            for j in range(3):
+                for c in range(2):
+                    ops.append((L[k][j][c].slot, (6 * nsteps) * k + 6 * step + 2 * j + c))
+        return ops
+
+    first = True
+    for s, kind in enumerate(kinds):
+        ld = loads(s)
+        if first:
+            # f = 1 (set by the prologue): load both lines, then f = L1 * L2 via two sparse products
+            p.round([Op(dst_of(f[0][0]), [], [(f[0][0].slot, 1)], load=ld[0])] +
+                    [Op(dst_of(f[i // 2][i % 2]), [], [(f[i // 2][i % 2].slot, 1)], load=ld[i]) for i in range(1, 12)])
+            first = False
+        elif kind == "dbl":
+            ops = fp12_sqr_ops(f, f)
+            for i, o in enumerate(ops):
+                o.load = ld[i]
+            p.round(ops)
+        else:
+            # addition step: no squaring; the loads ride on an identity round
+            p.round([Op(dst_of(f[i // 2][i % 2]), [], [(f[i // 2][i % 2].slot, 1)], load=ld[i]) for i in range(12)])
+        p.round(fp12_mul_line_ops(f, L[0], f))
+        p.round(fp12_mul_line_ops(f, L[1], f))
+    # x < 0: f -> conj(f)
+    p.round(copy_ops(flat12(conj12(f)), flat12(f)))
+    return p
+
+
+# ============================================================================ final exponentiation
+FROB = None
+
+
+def _fp2_pow(a, e):
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = ((r[0] * a[0] - r[1] * a[1]) % P, (r[0] * a[1] + r[1] * a[0]) % P)
+        a = ((a[0] * a[0] - a[1] * a[1]) % P, (2 * a[0] * a[1]) % P)
+        e >>= 1
+    return r
+
+
+def frob_consts():
+    global FROB
+    if FROB is None:
+        FROB = {k: [_fp2_pow((1, 1), i * (P ** k - 1) // 6) for i in range(6)] for k in (1, 2)}
+    return FROB
+
+
+def frob_ops(p, a, k, out):
+    """out = a^(p^k): out_i = conj^k(a_i) * gamma_{k,i}."""
+    g = frob_consts()[k]
+    ops = []
+    for i in range(6):
+        x0, x1 = a[i]
+        if k % 2:
+            x1 = ~x1
+        for comp in range(2):
+            if i == 0:
+                src = (x0, x1)[comp]
+                ops.append(Op(dst_of(out[i][comp]), [], [(src.slot, -1 if src.neg else 1)]))
+                continue
+            c0, c1 = g[i]
+            cv = (T(p.const(c0)), T(p.const(c1)))
+            prods = fp2_prod((x0, x1), cv, comp)
+            if c1 == 0:
+                prods = [pr for pr in prods if pr[1][0].slot != cv[1].slot]
+            ops.append(Op(dst_of(out[i][comp]), prods))
+    return ops
+
+
+def fexp_program(team=12):
+    """f^((p^12 - 1)/r) * 3 exactly as gen_programs.fexp_program (result e^3): easy part
+    (p^6 - 1)(p^2 + 1) with a team-parallel Fp12 inversion, hard part (x-1)^2 (x+p)(x^2+p^2-1) + 3."""
+    p = Program("fexp", team)
+    f = fp12_slots(p, "f")
+    c0 = [f[0], f[2], f[4]]   # Fp6 halves in the v basis
+    c1 = [f[1], f[3], f[5]]
+    # ---- t = c0^2 - v c1^2
+    t = [slots2(p) for _ in range(3)]
+    ops = []
+    for comp in range(2):
+        a, b = c0, c1
+        ops.append(Op(dst_of(t[0][comp]), fp2_sqr(a[0], comp) + fp2_prod(a[1], a[2], comp, True, 2) +
+                      fp2_sqr(b[1], comp, True, -1) + fp2_prod(b[0], b[2], comp, True, -2)))
+        ops.append(Op(dst_of(t[1][comp]), fp2_prod(a[0], a[1], comp, False, 2) + fp2_sqr(a[2], comp, True) +
+                      fp2_sqr(b[0], comp, False, -1) + fp2_prod(b[1], b[2], comp, True, -2)))
+        ops.append(Op(dst_of(t[2][comp]), fp2_sqr(a[1], comp) + fp2_prod(a[0], a[2], comp, False, 2) +
+                      fp2_prod(b[0], b[1], comp, False, -2) + fp2_sqr(b[2], comp, True, -1)))
+    p.round(ops)
+    # ---- s = adj(t): s0 = t0^2 - xi t1 t2, s1 = xi t2^2 - t0 t1, s2 = t1^2 - t0 t2
+    s = [slots2(p) for _ in range(3)]
+    ops = []
+    for comp in range(2):
+        ops.append(Op(dst_of(s[0][comp]), fp2_sqr(t[0], comp) + fp2_prod(t[1], t[2], comp, True, -1)))
+        ops.append(Op(dst_of(s[1][comp]), fp2_sqr(t[2], comp, True) + fp2_prod(t[0], t[1], comp, False, -1)))
+        ops.append(Op(dst_of(s[2][comp]), fp2_sqr(t[1], comp) + fp2_prod(t[0], t[2], comp, False, -1)))
+    p.round(ops)
+    # ---- d = t0 s0 + xi (t2 s1 + t1 s2)
+    d = slots2(p)
+    p.round([Op(dst_of(d[c]), fp2_prod(t[0], s[0], c) + fp2_prod(t[2], s[1], c, True) +
+                fp2_prod(t[1], s[2], c, True)) for c in range(2)])
+    # ---- n = d0^2 + d1^2 ; ninv
+    n = T(p.alloc())
+    p.round([Op(n.slot, [([d[0]], [d[0]], 1), ([d[1]], [d[1]], 1)])])
+    ninv = T(p.alloc())
+    p.round([Op(ninv.slot, [], [(n.slot, 1)], kind="inv")])
+    # ---- dinv = (d0 ninv, -d1 ninv) ; tinv = s * dinv
+    dinv = slots2(p)
+    p.round([Op(dst_of(dinv[0]), [([d[0]], [ninv], 1)]), Op(dst_of(dinv[1]), [([d[1]], [ninv], -1)])])
+    ti = [slots2(p) for _ in range(3)]
+    p.round([Op(dst_of(ti[i][c]), fp2_prod(s[i], dinv, c)) for i in range(3) for c in range(2)])
+    # ---- finv = (c0 * ti, -c1 * ti)   (Fp6 products)
+    fi = fp12_slots(p)
+    fi0 = [fi[0], fi[2], fi[4]]
+    fi1 = [fi[1], fi[3], fi[5]]
+    ops = []
+    for half, src, sign in ((fi0, c0, 1), (fi1, c1, -1)):
+        for k in range(3):
+            for comp in range(2):
+                prods = []
+                for i in range(3):
+                    j = (k - i) % 3
+                    prods += fp2_prod(src[i], ti[j], comp, xi=(i + j >= 3), m=sign)
+                ops.append(Op(dst_of(half[k][comp]), prods))
+    p.round(ops)
+    # ---- t1 = conj(f) * finv ; m = frob2(t1) * t1   (then everything of the easy part is dead)
+    t1 = fp12_slots(p)
+    p.round(fp12_mul_ops(conj12(f), fi, t1))
+    fr = fp12_slots(p)
+    p.round(frob_ops(p, t1, 2, fr))
+    m = fp12_slots(p, "m")
+    p.round(fp12_mul_ops(fr, t1, m))
+    dead = flat12(f) + flat12(fi) + flat12(t1) + flat12(fr) + [x for v in t + s + ti for x in v] + list(d) + \
+        list(dinv) + [n, ninv]
+    p.release([x.slot for x in dead])
+    acc = fp12_slots(p)
+    tmp = fp12_slots(p)
+
+    def exp_x(a, out):
+        """out = a^|x| (a cyclotomic; `out` must differ from a's slots)."""
+        firstsq = True
+        for bit in bin(X_ABS)[3:]:
+            p.round(cyclo_sqr_ops(a if firstsq else out, out))
+            firstsq = False
+            if bit == "1":
+                p.round(fp12_mul_ops(out, a, out))
+
+    # A = conj(exp_x(m) * m)
+    exp_x(m, acc)
+    A = fp12_slots(p)
+    p.round(fp12_mul_ops(acc, m, A))
+    A = conj12(A)
+    # A2 = conj(exp_x(A) * A)
+    exp_x(A, acc)
+    A2 = fp12_slots(p)
+    p.round(fp12_mul_ops(acc, A, A2))
+    p.release([x.slot for x in flat12(A)])
+    A2 = conj12(A2)
+    # Bv = conj(exp_x(A2)) * frob1(A2)
+    exp_x(A2, acc)
+    p.round(frob_ops(p, A2, 1, tmp))
+    Bv = fp12_slots(p)
+    p.round(fp12_mul_ops(conj12(acc), tmp, Bv))
+    p.release([x.slot for x in flat12(A2)])
+    # t = exp_x(exp_x(Bv))
+    exp_x(Bv, acc)
+    exp_x(acc, tmp)          # tmp = exp_x(acc)
+    # C = t * frob2(Bv) * conj(Bv)
+    p.round(frob_ops(p, Bv, 2, acc))           # acc = frob2(Bv)
+    C = fp12_slots(p)
+    p.round(fp12_mul_ops(tmp, acc, C))
+    p.round(fp12_mul_ops(C, conj12(Bv), C))
+    # r = C * (cyclo_sqr(m) * m)
+    p.round(cyclo_sqr_ops(m, acc))
+    p.round(fp12_mul_ops(acc, m, acc))
+    p.release([x.slot for x in flat12(Bv) + flat12(tmp)])
+    r = fp12_slots(p, "r")
+    p.round(fp12_mul_ops(C, acc, r))
+    return p
+
+
+# ============================================================================ checks against the oracle
+def _f12_from_mem(p, mem, name):
+    g = [(unmont(mem[p.named[f"{name}{i}_0"]]), unmont(mem[p.named[f"{name}{i}_1"]])) for i in range(6)]
+    return g
+
+
+def run_miller(lp, ap, Pp, Q):
+    """Emulate: both line programs, then the accumulation; returns the Fp12 coefficients (canonical)."""
+    lines = {}
+    for k, (pt, q) in enumerate(zip(Pp, Q)):
+        mem = {}
+        (qx0, qx1), (qy0, qy1) = q
+        for nm, v in (("qx0", qx0), ("qx1", qx1), ("qy0", qy0), ("qy1", qy1), ("tx0", qx0), ("tx1", qx1),
+                      ("ty0", qy0), ("ty1", qy1), ("tz0", 1), ("tz1", 0), ("nxp", (-pt[0]) % P), ("yp", pt[1])):
+            mem[lp.named[nm]] = mont(v)
+        for s in range(lp.nslots):
+            mem.setdefault(s, 0)
+        out = {}
+        lp.emulate(mem, io_out=out)
+        for idx, v in out.items():
+            lines[6 * lp.nsteps * k + idx] = v
+    mem = {s: 0 for s in range(ap.nslots)}
+    mem[ap.named["f0_0"]] = mont(1)
+    ap.emulate(mem, io_in=lines)
+    return _f12_from_mem(ap, mem, "f")
+
+
+def check_miller(lp, ap):
+    from oracle import bls12_381 as B
+    rnd = random.Random(7)
+    for _ in range(2):
+        a, b = rnd.randrange(1, 1 << 60), rnd.randrange(1, 1 << 60)
+        P1 = B.g1_mul(B.G1_GEN, a)
+        Q1 = B.g2_mul(B.G2_GEN, b)
+        Q2 = B.g2_mul(B.G2_GEN, b + 7)
+        P2 = B.g1_neg(B.G1_GEN)
+        g = run_miller(lp, ap, [P1, P2], [Q1, Q2])
+        got = B.final_exponentiation(B.f12_from_coeffs(g))
+        exp = B.f12_mul(B.pairing(P1, Q1), B.pairing(P2, Q2))
+        assert got == exp, "SOP miller mismatch"
+    print("  SOP Miller (lines + accumulation) checked against oracle pairings")
+
+
+def check_fexp(fp):
+    from oracle import bls12_381 as B
+    rnd = random.Random(9)
+    f = tuple(tuple((rnd.randrange(P), rnd.randrange(P)) for _ in range(3)) for _ in range(2))
+    g = B.f12_coeffs(f)
+    mem = {s: 0 for s in range(fp.nslots)}
+    for i in range(6):
+        mem[fp.named[f"f{i}_0"]], mem[fp.named[f"f{i}_1"]] = mont(g[i][0]), mont(g[i][1])
+    fp.emulate(mem)
+    out = _f12_from_mem(fp, mem, "r")
+    e = B.final_exponentiation(f)
+    assert B.f12_from_coeffs(out) == B.f12_mul(B.f12_mul(e, e), e), "SOP fexp mismatch"
+    print("  SOP final exponentiation checked against the oracle (e^3)")
+
+
+# ============================================================================ emit
+def emit(progs, path):
+    lines = ["// GENERATED by tools/gen_sop.py — do not edit.  SOP team programs (see lcv_sop.hpp).",
+             "#pragma once", "#include <stdint.h>", ""]
+    for p in progs:
+        hdr, rec = p.encode()
+        N = p.name.upper()
+        lines.append(f"// {p.stats()}")
+        lines.append(f"#define LCV_SOP_{N}_TEAM {p.team}")
+        lines.append(f"#define LCV_SOP_{N}_ROUNDS {len(hdr) // 4}")
+        lines.append(f"#define LCV_SOP_{N}_SLOTS {p.nslots}")
+        lines.append(f"#define LCV_SOP_{N}_NCONST {len(p.consts)}")
+        lines.append(f"#define LCV_SOP_{N}_MAXK {max(max(len(o.prods) for o in r) for r in p.rounds)}")
+        if hasattr(p, "nsteps"):
+            lines.append(f"#define LCV_SOP_{N}_NSTEPS {p.nsteps}")
+        for nm, s in sorted(p.named.items(), key=lambda kv: kv[1]):
+            lines.append(f"#define LCV_SOP_{N}_SLOT_{nm.upper()} {s}")
+        lines.append(f"static const uint32_t kSop_{p.name}_hdr[{len(hdr)}] = {{")
+        for i in range(0, len(hdr), 16):
+            lines.append("  " + ",".join(str(w) for w in hdr[i:i + 16]) + ",")
+        lines.append("};")
+        lines.append(f"static const uint32_t kSop_{p.name}_rec[{len(rec)}] = {{")
+        for i in range(0, len(rec), 16):
+            lines.append("  " + ",".join(str(w) for w in rec[i:i + 16]) + ",")
+        lines.append("};")
+        lines.append(f"static const uint32_t kSop_{p.name}_consts[{max(1, len(p.consts)) * 12}] = {{")
+        for c in p.const_list() or [0]:
+            mv = mont(c)
+            lines.append("  " + ",".join(f"0x{(mv >> (32 * k)) & 0xffffffff:08x}u" for k in range(12)) + ",")
+        lines.append("};")
+        lines.append("")
+    open(path, "w").write("\n".join(lines) + "\n")
+
+
+def build():
+    lp = line_program()
+    ap = acc_program(nsteps=lp.nsteps)
+    fp = fexp_program()
+    return lp, ap, fp
+
+
+def main():
+    ap_ = argparse.ArgumentParser()
+    ap_.add_argument("--check", action="store_true")
+    ap_.add_argument("--out", default=os.path.join(ROOT, "light-client-consensus-specs_amd", "csrc",
+                                                  "lcv_sop_programs.inc"))
+    args = ap_.parse_args()
+    progs = build()
+    for p in progs:
+        p.finalize()
+        print(p.stats())
+    if args.check:
+        check_miller(progs[0], progs[1])
+        check_fexp(progs[2])
+    emit(progs, args.out)
+
+
+if __name__ == "__main__":
+    main()
