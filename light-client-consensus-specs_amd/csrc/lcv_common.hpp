@@ -36,10 +36,11 @@
 #endif
 
 // Op counting (test-only host-simulation build with -DLCV_OPCOUNT): Fp multiplications, Fp
-// additions/subtractions/halvings and SHA-256 compressions, per stage -> the roofline numerator.
+// additions/subtractions/halvings, SHA-256 compressions and (3) SOP-engine 12x12-limb products or
+// Montgomery reductions (each half of a reduced Fp multiplication), per stage -> the roofline numerator.
 #if defined(LCV_HOSTSIM) && defined(LCV_OPCOUNT)
 #include <atomic>
-namespace lcv { extern std::atomic<unsigned long long> g_ops[3]; }
+namespace lcv { extern std::atomic<unsigned long long> g_ops[4]; }
 #define LCV_COUNT(k) ((void)lcv::g_ops[k].fetch_add(1, std::memory_order_relaxed))
 #else
 #define LCV_COUNT(k) ((void)0)

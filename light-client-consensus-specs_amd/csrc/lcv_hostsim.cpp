@@ -18,7 +18,7 @@
 struct lcv_ctx;
 
 #ifdef LCV_OPCOUNT
-namespace lcv { std::atomic<unsigned long long> g_ops[3]; }
+namespace lcv { std::atomic<unsigned long long> g_ops[4]; }
 #endif
 
 // Stage marks are kept per (simulated) stream, like the HIP backend's, so that marks opened on
@@ -27,8 +27,8 @@ struct Backend {
   int cur = 0;
   int open_stage[4] = {-1, -1, -1, -1};
   std::chrono::steady_clock::time_point t0[4];
-  unsigned long long ops0[4][3] = {};
-  unsigned long long ops[16][3] = {};
+  unsigned long long ops0[4][4] = {};
+  unsigned long long ops[16][4] = {};
   // test-only stand-in for the RCCL communicator: collectives through files in a directory shared by
   // the ranks (the "unique id" is its path), so the multi-process path runs on the CPU (tests/test_multi.py)
   std::string comm_dir;
@@ -124,7 +124,7 @@ static void be_stage_begin(lcv_ctx* ctx, int stage) {
   b.open_stage[b.cur] = stage;
   b.t0[b.cur] = std::chrono::steady_clock::now();
 #ifdef LCV_OPCOUNT
-  for (int k = 0; k < 3; ++k) b.ops0[b.cur][k] = lcv::g_ops[k].load();
+  for (int k = 0; k < 4; ++k) b.ops0[b.cur][k] = lcv::g_ops[k].load();
 #endif
 }
 static void be_stage_end(lcv_ctx* ctx, int stage) {
@@ -133,14 +133,14 @@ static void be_stage_end(lcv_ctx* ctx, int stage) {
   const auto t1 = std::chrono::steady_clock::now();
   ctx->stage_ms[stage] += std::chrono::duration<float, std::milli>(t1 - b.t0[b.cur]).count();
 #ifdef LCV_OPCOUNT
-  for (int k = 0; k < 3; ++k) b.ops[stage][k] += lcv::g_ops[k].load() - b.ops0[b.cur][k];
+  for (int k = 0; k < 4; ++k) b.ops[stage][k] += lcv::g_ops[k].load() - b.ops0[b.cur][k];
 #endif
   b.open_stage[b.cur] = -1;
 }
 static void be_reset_timings(lcv_ctx* ctx) {
   for (int k = 0; k < 4; ++k) ctx->be.open_stage[k] = -1;
   for (int s = 0; s < ST_COUNT; ++s) ctx->stage_ms[s] = 0.f;
-  for (int s = 0; s < 16; ++s) for (int k = 0; k < 3; ++k) ctx->be.ops[s][k] = 0;
+  for (int s = 0; s < 16; ++s) for (int k = 0; k < 4; ++k) ctx->be.ops[s][k] = 0;
 }
 static void be_collect_timings(lcv_ctx*) {}
 
@@ -201,10 +201,11 @@ extern "C" int lcv_device_count(int* out) {
 }
 
 // test/tool-only: per-stage operation counts of the last validate call (needs -DLCV_OPCOUNT):
-// out[3 * s + k], k = 0 Fp multiplications, 1 Fp additions/subtractions/halvings, 2 SHA-256 compressions
+// out[4 * s + k], k = 0 Fp multiplications, 1 Fp additions/subtractions/halvings, 2 SHA-256 compressions,
+// 3 SOP half-multiplications (a 12x12-limb product or a Montgomery reduction)
 extern "C" int lcv_debug_opcounts(lcv_ctx* ctx, unsigned long long* out, int max_stages) {
   if (!ctx || !out) return LCV_EINVAL;
   for (int s = 0; s < max_stages && s < 16; ++s)
-    for (int k = 0; k < 3; ++k) out[3 * s + k] = ctx->be.ops[s][k];
+    for (int k = 0; k < 4; ++k) out[4 * s + k] = ctx->be.ops[s][k];
   return LCV_OK;
 }

@@ -44,15 +44,16 @@ def test_opcount_every_stage():
         assert per.get(st, {}).get("fp_mul", 0) > 0, st
     for st in ("pre_checks", "nsc_htr"):
         assert per[st]["sha"] > 0
-    # the programs' MUL counts are what the op counter sees (one per MUL op, not per lane)
-    # (+2 per inversion: the binary GCD's conversions out of / into Montgomery form)
-    import gen_programs as G
+    # the SOP programs' products and reductions are what the op counter sees (padding products excluded):
+    # each is half of a reduced Fp multiplication
+    import gen_sop as GS
+    lp, ap, fp = GS.build()
 
-    def muls(p):
-        ops = [v for r in p.rounds for v in r]
-        return sum(v.kind == "mul" for v in ops) + 2 * sum(v.kind == "inv" for v in ops)
-    assert per["final_exp"]["fp_mul"] == muls(G.make_fexp(16))
-    assert per["miller_loop"]["fp_mul"] == muls(G.make_miller(32))
+    def half_muls(p):
+        return sum(len(o.prods) + 1 for r in p.rounds for o in r) / 2
+    assert per["final_exp"]["fp_mul"] == half_muls(fp) + 2  # + the inversion's Montgomery conversions
+    assert per["miller_loop"]["fp_mul"] == half_muls(ap)
+    assert per["miller_lines"]["fp_mul"] == 2 * half_muls(lp)
     tot = c["total_per_update"]
     assert abs(sum(d["fp_mul"] for d in per.values()) - tot["fp_mul"]) < 1e-6
 

@@ -33,11 +33,13 @@ def count(n: int = 8, participation: str = "full", npool: int = 1) -> dict:
     ok, _ = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
     assert ok.all()
     names = list(v.last_timings().keys())
-    buf = (C.c_ulonglong * (3 * len(names)))()
+    buf = (C.c_ulonglong * (4 * len(names)))()
     lib.dll.lcv_debug_opcounts(v.ctx, buf, len(names))
     per = {}
     for s, name in enumerate(names):
-        fm, fa, sh = buf[3 * s], buf[3 * s + 1], buf[3 * s + 2]
+        # an SOP half-multiplication (a 12x12-limb product or a Montgomery reduction) is half of a
+        # reduced Fp multiplication's 288 multiply-accumulates
+        fm, fa, sh = buf[4 * s] + buf[4 * s + 3] / 2, buf[4 * s + 1], buf[4 * s + 2]
         if fm or fa or sh:
             per[name] = {"fp_mul": fm / n, "fp_add": fa / n, "sha": sh / n,
                          "int32_ops": (600 * fm + 24 * fa + 2100 * sh) / n}
