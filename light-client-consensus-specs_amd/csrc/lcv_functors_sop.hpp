@@ -14,17 +14,20 @@ enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_V
 
 struct F_sop_lines {
   Work W; SopView P;
+  uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
-  // item t: update i = t >> 1, pairing k = t & 1 (k = 0: e(PK_agg, H(m)); k = 1: e(-G1, signature))
+  // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
+  LCV_HD uint32_t upd(uint32_t t) const { return mode == 0 ? t >> 1 : t; }
+  LCV_HD uint32_t pk(uint32_t t) const { return mode == 0 ? (t & 1u) : (mode == 1 ? 1u : 0u); }
   LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
   LCV_HD uint32_t* io_out(uint32_t t) const {
-    return W.lines + (size_t)(t >> 1) * SOP_LINE_WORDS + (size_t)(t & 1u) * SOP_LINE_VALS * 12;
+    return W.lines + (size_t)upd(t) * SOP_LINE_WORDS + (size_t)pk(t) * SOP_LINE_VALS * 12;
   }
   // T = (Qx, Qy, 1), Q affine; (-xP, yP).  An identity Q becomes (G2 generator, P = (0, 0)): constant
   // lines, killed by the final exponentiation (e(P, O) = 1).
   LCV_HD void prologue(uint32_t t, uint32_t lane, uint32_t* lds) const {
-    const uint32_t i = t >> 1, k = t & 1u;
+    const uint32_t i = upd(t), k = pk(t);
     const bool id = k == 0 ? W.qh_inf[i] != 0 : W.sig_status[i] != PT_OK;
     for (uint32_t v = lane; v < 12; v += TEAM) {
       fp x;
@@ -64,7 +67,20 @@ struct F_sop_lines {
       LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * slot + j] = x.v[j];
     }
   }
-  LCV_HD void epilogue(uint32_t, uint32_t, const uint32_t*) const {}
+  // the signature pairing's walk ends at T = [|x|]Q: the G2 subgroup check of the signature
+  // (psi(Q) == [x]Q, program rounds e1/e2) turns PT_OK into PT_BAD for a non-member
+  LCV_HD void epilogue(uint32_t t, uint32_t lane, const uint32_t* lds) const {
+    if (lane != 0 || pk(t) != 1u) return;
+    const uint32_t i = upd(t);
+    if (W.sig_status[i] != PT_OK) return;
+    uint32_t e = 0, z = 0;
+    for (int j = 0; j < 12; ++j) {
+      e |= lds[12 * LCV_SOP_LINES_SLOT_E10 + j] | lds[12 * LCV_SOP_LINES_SLOT_E11 + j] |
+           lds[12 * LCV_SOP_LINES_SLOT_E20 + j] | lds[12 * LCV_SOP_LINES_SLOT_E21 + j];
+      z |= lds[12 * LCV_SOP_LINES_SLOT_TZ0 + j] | lds[12 * LCV_SOP_LINES_SLOT_TZ1 + j];
+    }
+    if (e != 0 || z == 0) W.sig_status[i] = PT_BAD;
+  }
 };
 
 struct F_sop_acc {
@@ -129,7 +145,7 @@ struct F_sop_fexp {
 // idle.  The round header is wave-uniform (scalar loads); each lane reads its record from global
 // memory (L2-resident program).  Blocks are one wave, so the barrier between rounds is a wave barrier.
 template <class F>
-__global__ __launch_bounds__(64) void k_sop(F f, uint32_t n) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_sop(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
   __shared__ uint32_t lds[F::SHARED_WORDS + G * F::LDS_WORDS];
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;

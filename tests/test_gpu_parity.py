@@ -116,3 +116,28 @@ def test_store_sequence_on_gpu(gpu_verifier):
     sequence (tests/golden/store_sequence.npz) step by step and in the batched form."""
     import store_cases
     store_cases.run(gpu_verifier)
+
+
+def test_validate_non_subgroup_signature(gpu_verifier):
+    """Signatures that decode to curve points outside G2 (or to the identity) fail at :464 on the
+    validate path, where the G2 subgroup check is fused into the signature pairing's line walk."""
+    from lcv import synth
+    sb = synth.generate(gpu_verifier, 6, seed=9)
+    sigs = sb.updates.sync_signature
+    x, bad = 1, []
+    while len(bad) < 3:
+        x += 1
+        X = (x, 11)
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(X), X), B.B2))
+        if y is not None and not B.g2_in_subgroup((X, y)):
+            bad.append(B.g2_compress((X, y)))
+    for row, s in zip((1, 3, 4), bad):
+        sigs[row] = np.frombuffer(s, np.uint8)
+    sigs[5] = np.frombuffer(bytes([0xC0]) + bytes(95), np.uint8)  # identity signature
+    gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    ok, reason = gpu_verifier.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    store = H.store_from(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    exp = [H.O.validate_light_client_update(store, H.update_from(sb.updates, i), sb.current_slot,
+                                            sb.genesis_validators_root) for i in range(6)]
+    assert exp == [0, 14, 0, 14, 14, 14]
+    assert list(reason) == exp

@@ -425,6 +425,17 @@ def flat12(f):
 
 
 # ============================================================================ Miller loop: lines
+PSI_CX = None
+PSI_CY = None
+
+
+def _psi_consts():
+    def inv2(a):
+        n = pow((a[0] * a[0] + a[1] * a[1]) % P, P - 2, P)
+        return (a[0] * n % P, (-a[1]) * n % P)
+    return inv2(_fp2_pow((1, 1), (P - 1) // 3)), inv2(_fp2_pow((1, 1), (P - 1) // 2))
+
+
 def line_program(team=10):
     """One pairing's T walk over |x| (63 doublings, 5 additions; the projective doubling of
     gen_programs.line_dbl scaled by 4, no halvings), emitting per step the sparse line
@@ -436,8 +447,19 @@ def line_program(team=10):
     B, Cp, J, XY, YZ = (slots2(p) for _ in range(5))
     BmF, BpF = slots2(p), slots2(p)
     la, lb, lc = slots2(p), slots2(p), slots2(p)
-    th, lam, Cc, D, E, F, G, H, GmH = (slots2(p) for _ in range(9))
+    # the addition step's temporaries reuse the doubling step's (different steps, sequential rounds)
+    th, lam, Cc, D, E, F, G = B, Cp, J, XY, YZ, BmF, BpF
+    H, GmH = slots2(p), slots2(p)
     one = T(p.const(1))
+    # G2 subgroup check of Q (Scott: psi(Q) == [x]Q): psi(Q) = (conj(qx) cx, conj(qy) cy) now; at the end
+    # T = [|x|]Q = -[x]Q, so Q is in G2 iff Z != 0, e1 = px Z - X = 0 and e2 = py Z + Y = 0.  The walk's
+    # formulas are exact on G2; on a non-member any exceptional case leaves Z = 0 for good (T = Q in an
+    # addition gives (0 : 0 : 0), T = -Q gives O, and O stays O), so a non-member is never accepted.
+    px, py = slots2(p, "px"), slots2(p, "py")
+    cx = (T(p.const(PSI_CX[0])), T(p.const(PSI_CX[1])))
+    cy = (T(p.const(PSI_CY[0])), T(p.const(PSI_CY[1])))
+    p.round([Op(dst_of(px[c]), fp2_prod((qx[0], ~qx[1]), cx, c)) for c in range(2)] +
+            [Op(dst_of(py[c]), fp2_prod((qy[0], ~qy[1]), cy, c)) for c in range(2)])
     step = 0
 
     for bit in bin(X_ABS)[3:]:
@@ -488,6 +510,9 @@ def line_program(team=10):
             ops += [Op(dst_of(Z[c]), fp2_prod(Z, E, c)) for c in range(2)]
             p.round(ops)
             step += 1
+    e1, e2 = slots2(p, "e1"), slots2(p, "e2")
+    p.round([Op(dst_of(e1[c]), fp2_prod(px, Z, c), [(X[c].slot, -1)]) for c in range(2)] +
+            [Op(dst_of(e2[c]), fp2_prod(py, Z, c), [(Y[c].slot, 1)]) for c in range(2)])
     p.nsteps = step
     return p
 
@@ -637,15 +662,16 @@ def fexp_program(team=12):
                     prods += fp2_prod(src[i], ti[j], comp, xi=(i + j >= 3), m=sign)
                 ops.append(Op(dst_of(half[k][comp]), prods))
     p.round(ops)
-    # ---- t1 = conj(f) * finv ; m = frob2(t1) * t1   (then everything of the easy part is dead)
-    t1 = fp12_slots(p)
-    p.round(fp12_mul_ops(conj12(f), fi, t1))
-    fr = fp12_slots(p)
-    p.round(frob_ops(p, t1, 2, fr))
-    m = fp12_slots(p, "m")
-    p.round(fp12_mul_ops(fr, t1, m))
-    dead = flat12(f) + flat12(fi) + flat12(t1) + flat12(fr) + [x for v in t + s + ti for x in v] + list(d) + \
-        list(dinv) + [n, ninv]
+    # ---- t1 = conj(f) * finv (in place over finv) ; m = frob2(t1) * t1 (frob2 into f's slots, m in place)
+    p.round(fp12_mul_ops(conj12(f), fi, fi))
+    t1 = fi
+    p.round(frob_ops(p, t1, 2, f))
+    p.round(fp12_mul_ops(f, t1, t1))
+    m = t1
+    for i in range(6):
+        for c in range(2):
+            p.named[f"m{i}_{c}"] = m[i][c].slot
+    dead = flat12(f) + [x for v in t + s + ti for x in v] + list(d) + list(dinv) + [n, ninv]
     p.release([x.slot for x in dead])
     acc = fp12_slots(p)
     tmp = fp12_slots(p)
@@ -659,37 +685,35 @@ def fexp_program(team=12):
             if bit == "1":
                 p.round(fp12_mul_ops(out, a, out))
 
-    # A = conj(exp_x(m) * m)
+    # A = conj(exp_x(m) * m)          (A in tmp)
     exp_x(m, acc)
-    A = fp12_slots(p)
-    p.round(fp12_mul_ops(acc, m, A))
-    A = conj12(A)
-    # A2 = conj(exp_x(A) * A)
+    p.round(fp12_mul_ops(acc, m, tmp))
+    A = conj12(tmp)
+    # A2 = conj(exp_x(A) * A)         (A2 in a fresh Fp12; A's slots become the next scratch)
     exp_x(A, acc)
-    A2 = fp12_slots(p)
-    p.round(fp12_mul_ops(acc, A, A2))
-    p.release([x.slot for x in flat12(A)])
-    A2 = conj12(A2)
-    # Bv = conj(exp_x(A2)) * frob1(A2)
+    A2s = fp12_slots(p)
+    p.round(fp12_mul_ops(acc, A, A2s))
+    A2 = conj12(A2s)
+    # Bv = conj(exp_x(A2)) * frob1(A2)  (frob1 into tmp, Bv in place over tmp)
     exp_x(A2, acc)
     p.round(frob_ops(p, A2, 1, tmp))
-    Bv = fp12_slots(p)
-    p.round(fp12_mul_ops(conj12(acc), tmp, Bv))
-    p.release([x.slot for x in flat12(A2)])
-    # t = exp_x(exp_x(Bv))
+    p.round(fp12_mul_ops(conj12(acc), tmp, tmp))
+    Bv = tmp
+    # t = exp_x(exp_x(Bv))             (t in A2's slots)
     exp_x(Bv, acc)
-    exp_x(acc, tmp)          # tmp = exp_x(acc)
-    # C = t * frob2(Bv) * conj(Bv)
-    p.round(frob_ops(p, Bv, 2, acc))           # acc = frob2(Bv)
-    C = fp12_slots(p)
-    p.round(fp12_mul_ops(tmp, acc, C))
-    p.round(fp12_mul_ops(C, conj12(Bv), C))
-    # r = C * (cyclo_sqr(m) * m)
+    exp_x(acc, A2s)
+    # C = t * frob2(Bv) * conj(Bv)     (frob2 into acc, C in place over A2s)
+    p.round(frob_ops(p, Bv, 2, acc))
+    p.round(fp12_mul_ops(A2s, acc, A2s))
+    p.round(fp12_mul_ops(A2s, conj12(Bv), A2s))
+    C = A2s
+    # r = C * (cyclo_sqr(m) * m)       (r over m's slots)
     p.round(cyclo_sqr_ops(m, acc))
     p.round(fp12_mul_ops(acc, m, acc))
-    p.release([x.slot for x in flat12(Bv) + flat12(tmp)])
-    r = fp12_slots(p, "r")
-    p.round(fp12_mul_ops(C, acc, r))
+    p.round(fp12_mul_ops(C, acc, m))
+    for i in range(6):
+        for c in range(2):
+            p.named[f"r{i}_{c}"] = m[i][c].slot
     return p
 
 
@@ -699,17 +723,30 @@ def _f12_from_mem(p, mem, name):
     return g
 
 
+def _line_inputs(lp, pt, q):
+    mem = {}
+    (qx0, qx1), (qy0, qy1) = q
+    for nm, v in (("qx0", qx0), ("qx1", qx1), ("qy0", qy0), ("qy1", qy1), ("tx0", qx0), ("tx1", qx1),
+                  ("ty0", qy0), ("ty1", qy1), ("tz0", 1), ("tz1", 0), ("nxp", (-pt[0]) % P), ("yp", pt[1])):
+        mem[lp.named[nm]] = mont(v)
+    for s in range(lp.nslots):
+        mem.setdefault(s, 0)
+    return mem
+
+
+def subgroup_emulated(lp, q):
+    mem = _line_inputs(lp, (1, 2), q)
+    lp.emulate(mem, io_out={})
+    e = [mem[lp.named[k]] for k in ("e10", "e11", "e20", "e21")]
+    z = [mem[lp.named[k]] for k in ("tz0", "tz1")]
+    return any(z) and not any(e)
+
+
 def run_miller(lp, ap, Pp, Q):
     """Emulate: both line programs, then the accumulation; returns the Fp12 coefficients (canonical)."""
     lines = {}
     for k, (pt, q) in enumerate(zip(Pp, Q)):
-        mem = {}
-        (qx0, qx1), (qy0, qy1) = q
-        for nm, v in (("qx0", qx0), ("qx1", qx1), ("qy0", qy0), ("qy1", qy1), ("tx0", qx0), ("tx1", qx1),
-                      ("ty0", qy0), ("ty1", qy1), ("tz0", 1), ("tz1", 0), ("nxp", (-pt[0]) % P), ("yp", pt[1])):
-            mem[lp.named[nm]] = mont(v)
-        for s in range(lp.nslots):
-            mem.setdefault(s, 0)
+        mem = _line_inputs(lp, pt, q)
         out = {}
         lp.emulate(mem, io_out=out)
         for idx, v in out.items():
@@ -733,7 +770,18 @@ def check_miller(lp, ap):
         got = B.final_exponentiation(B.f12_from_coeffs(g))
         exp = B.f12_mul(B.pairing(P1, Q1), B.pairing(P2, Q2))
         assert got == exp, "SOP miller mismatch"
-    print("  SOP Miller (lines + accumulation) checked against oracle pairings")
+    # the fused G2 subgroup check: members and non-members of G2
+    cases = [(B.g2_mul(B.G2_GEN, rnd.randrange(1, B.R)), True)]
+    x = 1
+    while len(cases) < 4:
+        x += 1
+        X = (x, 5)
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(X), X), B.B2))
+        if y is not None:
+            cases.append(((X, y), False))
+    for q, want in cases:
+        assert subgroup_emulated(lp, q) == want == B.g2_in_subgroup(q), "SOP subgroup check mismatch"
+    print("  SOP Miller (lines + accumulation) checked against oracle pairings; fused G2 subgroup check too")
 
 
 def check_fexp(fp):
@@ -786,6 +834,8 @@ def emit(progs, path):
 
 
 def build():
+    global PSI_CX, PSI_CY
+    PSI_CX, PSI_CY = _psi_consts()
     lp = line_program()
     ap = acc_program(nsteps=lp.nsteps)
     fp = fexp_program()
