@@ -140,14 +140,46 @@ struct F_sop_fexp {
   }
 };
 
+// hash_to_G2 tail after the two SSWU maps (W.qmap): isogeny, addition, cofactor clearing (complete
+// formulas), affine H(m) -> W.qh and its identity flag -> W.qh_inf
+struct F_sop_h2c {
+  Work W; SopView P;
+  static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12,
+                            SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
+  static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
+  static_assert(LCV_SOP_H2C_SLOT_HY1 == LCV_SOP_H2C_SLOT_HX0 + 3, "hx, hy in consecutive slots");
+  LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
+  LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
+  LCV_HD void prologue(uint32_t i, uint32_t lane, uint32_t* lds) const {
+    for (uint32_t v = lane; v < 8; v += TEAM) {
+      fp x;
+      soa_ld_fp(x, W.qmap, W.cap, i, v);
+      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * v + j] = x.v[j];
+    }
+  }
+  LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {
+    if (lane < 4) {
+      fp x;
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = lds[12 * (LCV_SOP_H2C_SLOT_HX0 + lane) + j];
+      soa_st_fp(W.qh, W.cap, i, lane, x);
+    } else if (lane == 4) {
+      uint32_t z = 0;
+      for (int j = 0; j < 12; ++j) z |= lds[12 * LCV_SOP_H2C_SLOT_HZ0 + j] | lds[12 * LCV_SOP_H2C_SLOT_HZ1 + j];
+      W.qh_inf[i] = z == 0 ? 1 : 0;
+    }
+  }
+};
+
 #ifdef LCV_KERNEL_UNIT
 // The SOP round loop: one wave per block, 64 / TEAM teams (items) per wave, lanes past the last team
 // idle.  The round header is wave-uniform (scalar loads); each lane reads its record from global
 // memory (L2-resident program).  Blocks are one wave, so the barrier between rounds is a wave barrier.
 template <class F>
+// LDS is dynamic (sized at launch): with a static size the compiler derives its occupancy target from
+// a smaller LDS than gfx950's 160 KB and gives the kernel 256 VGPRs (2 waves/SIMD).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_sop(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
-  __shared__ uint32_t lds[F::SHARED_WORDS + G * F::LDS_WORDS];
+  extern __shared__ uint32_t lds[];
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
   const uint32_t item = blockIdx.x * G + team;
   const bool active = team < G && item < n;

@@ -7,3 +7,4 @@
 LCV_INSTANTIATE_SOP(F_sop_lines)
 LCV_INSTANTIATE_SOP(F_sop_acc)
 LCV_INSTANTIATE_SOP(F_sop_fexp)
+LCV_INSTANTIATE_SOP(F_sop_h2c)

@@ -55,7 +55,8 @@ template <class F> __global__ void k_sop(F f, uint32_t n);
 template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s) {
   constexpr uint32_t G = 64 / F::TEAM;
   const uint32_t blocks = (n + G - 1) / G;
-  hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), 0, s, f, n);
+  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + G * F::LDS_WORDS);
+  hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), lds_bytes, s, f, n);
   return hipGetLastError();
 }
 #define LCV_INSTANTIATE_SOP(F) template hipError_t lcv_hip_launch_sop<F>(const F&, uint32_t, hipStream_t);

@@ -48,7 +48,7 @@ def test_opcount_every_stage():
     # the SOP programs' products and reductions are what the op counter sees (padding products excluded):
     # each is half of a reduced Fp multiplication
     import gen_sop as GS
-    lp, ap, fp = GS.build()
+    lp, ap, fp, _ = GS.build()
 
     def half_muls(p):
         return sum(len(o.prods) + 1 for r in p.rounds for o in r) / 2

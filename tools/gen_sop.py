@@ -78,7 +78,7 @@ class Op:
         self.dst = dst
         # a negative multiplier is folded into X's term signs: m > 0 from here on
         self.prods = [(list(x) if m > 0 else [~t for t in x], list(y), abs(int(m))) for x, y, m in prods]
-        self.adds = [(int(s), int(c)) for s, c in adds]
+        self.adds = [(s if isinstance(s, tuple) else int(s), int(c)) for s, c in adds]
         self.kind = kind
         self.load = load    # (ld_slot, io index): side-load of an Fp value from the program's input stream
         self.emit = emit    # io index: the result is also written to the program's output stream
@@ -717,6 +717,195 @@ def fexp_program(team=12):
     return p
 
 
+# ============================================================================ hash_to_G2 tail
+def _iso_consts():
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import gen_programs as GP
+    return GP.ISO_XNUM, GP.ISO_XDEN, GP.ISO_YNUM, GP.ISO_YDEN
+
+
+class G2Ops:
+    """Complete projective formulas on E2: y^2 = x^3 + 4(1 + u) (Renes-Costello-Batina 2016, a = 0,
+    b3 = 12(1 + u)) as SOP rounds: exact for every input (identity, P + P, P - P), so hash_to_G2 needs no
+    branches.  Points are (X, Y, Z) of Fp2 views; negation and psi's conjugations are views."""
+
+    def __init__(self, p):
+        self.p = p
+        self.t = [slots2(p) for _ in range(6)]   # round-1 products
+        self.u = [slots2(p) for _ in range(4)]   # round-2 linear combinations
+        self.one = T(p.const(1))
+
+    def dbl(self, P, out):
+        """out = 2P: t0 = Y^2, t1 = YZ, t2 = b3 Z^2, XY; X3 = 2 (t0 - 3 t2) XY, Y3 = t0^2 + 6 t0 t2 - 3 t2^2,
+        Z3 = 8 t0 t1.  Two rounds (8 + 6 lanes); `out` may be P (in place)."""
+        p = self.p
+        X, Y, Z = P
+        t0, t1, t2, xy = self.t[:4]
+        p.round([Op(dst_of(t0[c]), fp2_sqr(Y, c)) for c in range(2)] +
+                [Op(dst_of(t1[c]), fp2_prod(Y, Z, c)) for c in range(2)] +
+                [Op(dst_of(t2[c]), fp2_sqr(Z, c, xi=True, m=12)) for c in range(2)] +
+                [Op(dst_of(xy[c]), fp2_prod(X, Y, c)) for c in range(2)])
+        ops = [Op(dst_of(out[0][c]), fp2_prod(t0, xy, c, m=2) + fp2_prod(t2, xy, c, m=-6)) for c in range(2)]
+        ops += [Op(dst_of(out[1][c]), fp2_sqr(t0, c) + fp2_prod(t0, t2, c, m=6) + fp2_sqr(t2, c, m=-3))
+                for c in range(2)]
+        ops += [Op(dst_of(out[2][c]), fp2_prod(t0, t1, c, m=8)) for c in range(2)]
+        p.round(ops)
+
+    def add(self, P1, P2, out):
+        """out = P1 + P2 (RCB Alg. 7): three rounds (12, 8, 6 lanes); `out` may be P1 or P2."""
+        p = self.p
+        X1, Y1, Z1 = P1
+        X2, Y2, Z2 = P2
+        t0, t1, t2, t3, t4, y3 = self.t
+        ops = [Op(dst_of(t0[c]), fp2_prod(X1, X2, c)) for c in range(2)]
+        ops += [Op(dst_of(t1[c]), fp2_prod(Y1, Y2, c)) for c in range(2)]
+        ops += [Op(dst_of(t2[c]), fp2_prod(Z1, Z2, c)) for c in range(2)]
+        ops += [Op(dst_of(t3[c]), fp2_prod(X1, Y2, c) + fp2_prod(Y1, X2, c)) for c in range(2)]
+        ops += [Op(dst_of(t4[c]), fp2_prod(Y1, Z2, c) + fp2_prod(Z1, Y2, c)) for c in range(2)]
+        ops += [Op(dst_of(y3[c]), fp2_prod(X1, Z2, c) + fp2_prod(Z1, X2, c)) for c in range(2)]
+        p.round(ops)
+        z3, t1m, y3b, x3t = self.u
+        one = self.one
+        # b3 v = 12 (1 + u) v: (12 v0 - 12 v1, 12 v0 + 12 v1)
+        p.round([Op(dst_of(z3[0]), [([t1[0]], [one], 1)], [(t2[0].slot, 12), (t2[1].slot, -12)]),
+                 Op(dst_of(z3[1]), [([t1[1]], [one], 1)], [(t2[0].slot, 12), (t2[1].slot, 12)]),
+                 Op(dst_of(t1m[0]), [([t1[0]], [one], 1)], [(t2[0].slot, -12), (t2[1].slot, 12)]),
+                 Op(dst_of(t1m[1]), [([t1[1]], [one], 1)], [(t2[0].slot, -12), (t2[1].slot, -12)]),
+                 Op(dst_of(y3b[0]), [], [(y3[0].slot, 12), (y3[1].slot, -12)]),
+                 Op(dst_of(y3b[1]), [], [(y3[0].slot, 12), (y3[1].slot, 12)]),
+                 Op(dst_of(x3t[0]), [], [(t0[0].slot, 3)]),
+                 Op(dst_of(x3t[1]), [], [(t0[1].slot, 3)])])
+        ops = [Op(dst_of(out[0][c]), fp2_prod(t3, t1m, c) + fp2_prod(t4, y3b, c, m=-1)) for c in range(2)]
+        ops += [Op(dst_of(out[1][c]), fp2_prod(y3b, x3t, c) + fp2_prod(t1m, z3, c)) for c in range(2)]
+        ops += [Op(dst_of(out[2][c]), fp2_prod(z3, t4, c) + fp2_prod(x3t, t3, c)) for c in range(2)]
+        p.round(ops)
+
+    def mul_xabs(self, P, out):
+        """out = [|x|]P (out must not alias P)."""
+        first = True
+        for bit in bin(X_ABS)[3:]:
+            self.dbl(P if first else out, out)
+            first = False
+            if bit == "1":
+                self.add(out, P, out)
+
+    def psi(self, P, out):
+        """psi(X : Y : Z) = (conj(X) cx : conj(Y) cy : conj(Z)); the conj(Z) is a view of `out`'s Z."""
+        p = self.p
+        X, Y, Z = P
+        cx = (T(p.const(PSI_CX[0])), T(p.const(PSI_CX[1])))
+        cy = (T(p.const(PSI_CY[0])), T(p.const(PSI_CY[1])))
+        ops = [Op(dst_of(out[0][c]), fp2_prod((X[0], ~X[1]), cx, c)) for c in range(2)]
+        ops += [Op(dst_of(out[1][c]), fp2_prod((Y[0], ~Y[1]), cy, c)) for c in range(2)]
+        ops += copy_ops([Z[0], ~Z[1]], list(out[2]))
+        p.round(ops)
+
+
+def g2_neg_view(P):
+    return (P[0], neg2(P[1]), P[2])
+
+
+def g2_slots(p, name=None):
+    return tuple(slots2(p, f"{name}{c}" if name else None) for c in "xyz")
+
+
+def h2c_program(team=12):
+    """hash_to_G2 after the two SSWU maps (inputs: the affine E2' points m0, m1): 3-isogeny to E2 in
+    projective form (xn yd : y yn xd : xd yd), Q0 + Q1, clear_cofactor (RFC 9380 App. G.3:
+    [x^2 - x - 1]P + [x - 1] psi(P) + psi^2(2P), as gen_programs.h2c_program), then affine (hx, hy) and hz."""
+    p = Program("h2c", team)
+    XN, XD, YN, YD = _iso_consts()
+    m = [(slots2(p, f"m{k}x"), slots2(p, f"m{k}y")) for k in range(2)]
+    x2 = [slots2(p) for _ in range(2)]
+    x3 = [slots2(p) for _ in range(2)]
+    # powers of x
+    p.round([Op(dst_of(x2[k][c]), fp2_sqr(m[k][0], c)) for k in range(2) for c in range(2)])
+    p.round([Op(dst_of(x3[k][c]), fp2_prod(x2[k], m[k][0], c)) for k in range(2) for c in range(2)])
+    cst = lambda v: (T(p.const(v[0])), T(p.const(v[1])))  # noqa: E731
+
+    def poly_ops(k, cs, dst):
+        """sum_i cs[i] x^i with a monic top term (cs[-1] == (1, 0)) taken as an add-in."""
+        xp = {1: m[k][0], 2: x2[k], 3: x3[k]}
+        deg = len(cs) - 1
+        ops = []
+        for c in range(2):
+            prods, adds = [], []
+            for i in range(1, deg + 1):
+                if cs[i] == (1, 0):
+                    adds.append((xp[i][c].slot, 1))
+                elif cs[i] != (0, 0):
+                    prods += fp2_prod(cst(cs[i]), xp[i], c)
+            c0 = cs[0][c]
+            if c0:
+                adds.append((p.const(c0), 1))
+            assert len(adds) <= 2
+            ops.append(Op(dst_of(dst[c]), prods, adds))
+        return ops
+    xn, xd, yn, yd = ([slots2(p) for _ in range(2)] for _ in range(4))
+    p.round([o for k in range(2) for o in poly_ops(k, XN, xn[k]) + poly_ops(k, YN, yn[k])] +
+            [o for k in range(2) for o in poly_ops(k, XD, xd[k])])
+    p.round([o for k in range(2) for o in poly_ops(k, YD, yd[k])])
+    q = [g2_slots(p) for _ in range(2)]
+    yyn = [slots2(p) for _ in range(2)]
+    p.round([Op(dst_of(q[k][0][c]), fp2_prod(xn[k], yd[k], c)) for k in range(2) for c in range(2)] +
+            [Op(dst_of(q[k][2][c]), fp2_prod(xd[k], yd[k], c)) for k in range(2) for c in range(2)] +
+            [Op(dst_of(yyn[k][c]), fp2_prod(m[k][1], yn[k], c)) for k in range(2) for c in range(2)])
+    p.round([Op(dst_of(q[k][1][c]), fp2_prod(yyn[k], xd[k], c)) for k in range(2) for c in range(2)])
+    p.release([v.slot for grp in (x2, x3, xn, xd, yn, yd, yyn) for f2 in grp for v in f2] +
+              [v.slot for pt in m for f2 in pt for v in f2])
+    g = G2Ops(p)
+    Pt = g2_slots(p)
+    g.add(q[0], q[1], Pt)
+    # clear_cofactor: t1 = -[|x|]Pt, t2 = psi(Pt), t3 = psi^2(2 Pt) - t2, t2 = -[|x|](t1 + t2),
+    # Q = t3 + t2 - t1 - Pt
+    A = g2_slots(p)
+    g.mul_xabs(Pt, A)
+    t1 = g2_neg_view(A)
+    t2 = q[0]                       # q0, q1 are dead after Pt
+    g.psi(Pt, t2)
+    t3 = q[1]
+    g.dbl(Pt, t3)
+    g.psi(t3, t3)
+    g.psi(t3, t3)
+    g.add(t3, g2_neg_view(t2), t3)
+    g.add(t1, t2, t2)
+    B = g2_slots(p)
+    g.mul_xabs(t2, B)
+    g.add(t3, g2_neg_view(B), t3)
+    g.add(t3, g2_neg_view(t1), t3)
+    g.add(t3, g2_neg_view(Pt), t3)
+    X, Y, Z = t3
+    # affine: zi = Z^-1 via the norm
+    n, ninv = T(p.alloc()), T(p.alloc())
+    p.round([Op(n.slot, [([Z[0]], [Z[0]], 1), ([Z[1]], [Z[1]], 1)])])
+    p.round([Op(ninv.slot, [], [(n.slot, 1)], kind="inv")])
+    zi = slots2(p)
+    p.round([Op(dst_of(zi[0]), [([Z[0]], [ninv], 1)]), Op(dst_of(zi[1]), [([Z[1]], [ninv], -1)])])
+    hx, hy, hz = slots2(p, "hx"), slots2(p, "hy"), slots2(p, "hz")
+    p.round([Op(dst_of(hx[c]), fp2_prod(X, zi, c)) for c in range(2)] +
+            [Op(dst_of(hy[c]), fp2_prod(Y, zi, c)) for c in range(2)] + copy_ops(list(Z), list(hz)))
+    return p
+
+
+def check_h2c(hp):
+    from oracle import bls12_381 as B
+    rnd = random.Random(11)
+    for _ in range(2):
+        msg = rnd.randbytes(32)
+        u = B.hash_to_field_fp2(msg, 2, B.DST_POP)
+        mem = {s: 0 for s in range(hp.nslots)}
+        for k in range(2):
+            x, y = B.sswu_g2(u[k])
+            for nm, v in ((f"m{k}x0", x[0]), (f"m{k}x1", x[1]), (f"m{k}y0", y[0]), (f"m{k}y1", y[1])):
+                mem[hp.named[nm]] = mont(v)
+        hp.emulate(mem)
+        got = ((unmont(mem[hp.named["hx0"]]), unmont(mem[hp.named["hx1"]])),
+               (unmont(mem[hp.named["hy0"]]), unmont(mem[hp.named["hy1"]])))
+        assert got == B.hash_to_g2(msg), "SOP h2c mismatch"
+        assert mem[hp.named["hz0"]] or mem[hp.named["hz1"]]
+    print("  SOP hash_to_G2 tail checked against the oracle")
+
+
 # ============================================================================ checks against the oracle
 def _f12_from_mem(p, mem, name):
     g = [(unmont(mem[p.named[f"{name}{i}_0"]]), unmont(mem[p.named[f"{name}{i}_1"]])) for i in range(6)]
@@ -839,7 +1028,8 @@ def build():
     lp = line_program()
     ap = acc_program(nsteps=lp.nsteps)
     fp = fexp_program()
-    return lp, ap, fp
+    hp = h2c_program()
+    return lp, ap, fp, hp
 
 
 def main():
@@ -855,6 +1045,7 @@ def main():
     if args.check:
         check_miller(progs[0], progs[1])
         check_fexp(progs[2])
+        check_h2c(progs[3])
     emit(progs, args.out)
 
 
