@@ -152,7 +152,54 @@ LCV_FN void fp_mul_ps(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]
   t[11] = (uint32_t)acc;
   fp_reduce_once(r, t);
 }
-#define LCV_MUL_IMPL fp_mul_ps
+// The same product scanning with every column's products split over two independent accumulator
+// chains (even / odd i) merged at the column's end: one-lane-per-item kernels (a lone wave per SIMD,
+// latency-bound: F_h2c_map, F_sig) get two multiply-accumulates in flight instead of one.
+LCV_FN void mac_merge(uint64_t& acc, uint32_t& hi, uint64_t acc2, uint32_t hi2) {
+  uint32_t lo = (uint32_t)acc, mid = (uint32_t)(acc >> 32), c;
+  lo = addc32(lo, (uint32_t)acc2, 0u, c);
+  mid = addc32(mid, (uint32_t)(acc2 >> 32), c, c);
+  hi = hi + hi2 + c;
+  acc = ((uint64_t)mid << 32) | lo;
+}
+LCV_FN void fp_mul_ps2(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  uint32_t m[12], t[12];
+  uint64_t acc = 0, acc2;
+  uint32_t hi = 0, hi2;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) {
+    acc2 = 0;
+    hi2 = 0;
+    LCV_UNROLL for (int i = 0; i < k; ++i) {
+      if (i & 1) mac_vs(acc2, hi2, m[i], PL[k - i]);
+      else mac_vs(acc, hi, m[i], PL[k - i]);
+    }
+    LCV_UNROLL for (int i = 0; i <= k; ++i) {
+      if (i & 1) mac_vv(acc, hi, a[i], b[k - i]);
+      else mac_vv(acc2, hi2, a[i], b[k - i]);
+    }
+    mac_merge(acc, hi, acc2, hi2);
+    m[k] = (uint32_t)acc * LCV_NP0;
+    mac_vs(acc, hi, m[k], PL[0]);  // low word becomes 0
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  LCV_UNROLL for (int k = 12; k < 23; ++k) {
+    acc2 = 0;
+    hi2 = 0;
+    LCV_UNROLL for (int i = k - 11; i < 12; ++i) {
+      mac_vv(acc, hi, a[i], b[k - i]);
+      mac_vs(acc2, hi2, m[i], PL[k - i]);
+    }
+    mac_merge(acc, hi, acc2, hi2);
+    t[k - 12] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[11] = (uint32_t)acc;
+  fp_reduce_once(r, t);
+}
+#define LCV_MUL_IMPL fp_mul_ps2
 #elif defined(LCV_CPU_FAST)
 // CPU-baseline build only (liblcv_cpu.so, bench.py's cpu_baseline leg): the same Montgomery product
 // (R = 2^384, identical representation and results) on 6 x 64-bit limbs with 128-bit products, the

@@ -124,11 +124,19 @@ class Program:
         return ("c", self.consts[v])
 
     def round(self, ops):
+        """Append one round; more ops than lanes are split into consecutive rounds, which is only
+        exact when no op of a later part reads a slot an earlier part writes (checked)."""
         ops = [o for o in ops if o is not None]
-        assert 1 <= len(ops) <= self.team, (self.name, len(ops))
+        assert ops
         dsts = [o.dst for o in ops] + [o.load[0] for o in ops if o.load]
         assert len(dsts) == len(set(dsts)), "two ops of a round write one slot"
-        self.rounds.append(ops)
+        written = set()
+        for k in range(0, len(ops), self.team):
+            part = ops[k:k + self.team]
+            reads = {t.slot for o in part for x, y, _ in o.prods for t in x + y} | {s_ for o in part for s_, _ in o.adds}
+            assert not (reads & written), f"{self.name}: split round reads a slot an earlier part wrote"
+            written |= {o.dst for o in part}
+            self.rounds.append(part)
 
     # ------------------------------------------------------------ finalise: slot numbers of constants
     def finalize(self):
@@ -809,7 +817,7 @@ def g2_slots(p, name=None):
     return tuple(slots2(p, f"{name}{c}" if name else None) for c in "xyz")
 
 
-def h2c_program(team=12):
+def h2c_program(team=8):
     """hash_to_G2 after the two SSWU maps (inputs: the affine E2' points m0, m1): 3-isogeny to E2 in
     projective form (xn yd : y yn xd : xd yd), Q0 + Q1, clear_cofactor (RFC 9380 App. G.3:
     [x^2 - x - 1]P + [x - 1] psi(P) + psi^2(2P), as gen_programs.h2c_program), then affine (hx, hy) and hz."""
