@@ -152,54 +152,45 @@ LCV_FN void fp_mul_ps(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]
   t[11] = (uint32_t)acc;
   fp_reduce_once(r, t);
 }
-// The same product scanning with every column's products split over two independent accumulator
-// chains (even / odd i) merged at the column's end: one-lane-per-item kernels (a lone wave per SIMD,
-// latency-bound: F_h2c_map, F_sig) get two multiply-accumulates in flight instead of one.
-LCV_FN void mac_merge(uint64_t& acc, uint32_t& hi, uint64_t acc2, uint32_t hi2) {
-  uint32_t lo = (uint32_t)acc, mid = (uint32_t)(acc >> 32), c;
-  lo = addc32(lo, (uint32_t)acc2, 0u, c);
-  mid = addc32(mid, (uint32_t)(acc2 >> 32), c, c);
-  hi = hi + hi2 + c;
-  acc = ((uint64_t)mid << 32) | lo;
-}
-LCV_FN void fp_mul_ps2(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+// Squaring, product scanning: the cross products a_i a_j (i < j) of a column are accumulated once and
+// doubled (78 + 12 multiply-accumulates for the square instead of 144) — the windowed square-root
+// exponentiations of signature decoding and SSWU are ~80% squarings.
+LCV_FN void fp_sqr_ps(uint32_t r[12], const uint32_t a[12]) {
   constexpr uint32_t PL[12] = LCV_P_INIT;
   uint32_t m[12], t[12];
-  uint64_t acc = 0, acc2;
-  uint32_t hi = 0, hi2;
-  LCV_UNROLL for (int k = 0; k < 12; ++k) {
-    acc2 = 0;
-    hi2 = 0;
-    LCV_UNROLL for (int i = 0; i < k; ++i) {
-      if (i & 1) mac_vs(acc2, hi2, m[i], PL[k - i]);
-      else mac_vs(acc, hi, m[i], PL[k - i]);
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+  LCV_UNROLL for (int k = 0; k < 23; ++k) {
+    // cross terms of column k, doubled: 2 * sum_{i < j, i + j = k} a_i a_j
+    uint64_t x = 0;
+    uint32_t xh = 0;
+    LCV_UNROLL for (int i = (k > 11 ? k - 11 : 0); 2 * i < k; ++i) mac_vv(x, xh, a[i], a[k - i]);
+    {  // (xh:x) <<= 1, then acc += it
+      const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
+      const uint32_t d2 = (xh << 1) | (x1 >> 31), d1 = (x1 << 1) | (x0 >> 31), d0 = x0 << 1;
+      uint32_t lo = (uint32_t)acc, mid = (uint32_t)(acc >> 32), c;
+      lo = addc32(lo, d0, 0u, c);
+      mid = addc32(mid, d1, c, c);
+      hi = hi + d2 + c;
+      acc = ((uint64_t)mid << 32) | lo;
     }
-    LCV_UNROLL for (int i = 0; i <= k; ++i) {
-      if (i & 1) mac_vv(acc, hi, a[i], b[k - i]);
-      else mac_vv(acc2, hi2, a[i], b[k - i]);
+    if ((k & 1) == 0) mac_vv(acc, hi, a[k >> 1], a[k >> 1]);
+    if (k < 12) {
+      LCV_UNROLL for (int i = 0; i < k; ++i) mac_vs(acc, hi, m[i], PL[k - i]);
+      m[k] = (uint32_t)acc * LCV_NP0;
+      mac_vs(acc, hi, m[k], PL[0]);  // low word becomes 0
+    } else {
+      LCV_UNROLL for (int i = k - 11; i < 12; ++i) mac_vs(acc, hi, m[i], PL[k - i]);
+      t[k - 12] = (uint32_t)acc;
     }
-    mac_merge(acc, hi, acc2, hi2);
-    m[k] = (uint32_t)acc * LCV_NP0;
-    mac_vs(acc, hi, m[k], PL[0]);  // low word becomes 0
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
-  }
-  LCV_UNROLL for (int k = 12; k < 23; ++k) {
-    acc2 = 0;
-    hi2 = 0;
-    LCV_UNROLL for (int i = k - 11; i < 12; ++i) {
-      mac_vv(acc, hi, a[i], b[k - i]);
-      mac_vs(acc2, hi2, m[i], PL[k - i]);
-    }
-    mac_merge(acc, hi, acc2, hi2);
-    t[k - 12] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)hi << 32);
     hi = 0;
   }
   t[11] = (uint32_t)acc;
   fp_reduce_once(r, t);
 }
-#define LCV_MUL_IMPL fp_mul_ps2
+#define LCV_SQR_IMPL fp_sqr_ps
+#define LCV_MUL_IMPL fp_mul_ps
 #elif defined(LCV_CPU_FAST)
 // CPU-baseline build only (liblcv_cpu.so, bench.py's cpu_baseline leg): the same Montgomery product
 // (R = 2^384, identical representation and results) on 6 x 64-bit limbs with 128-bit products, the
@@ -275,7 +266,23 @@ LCV_FN void fp_mul(fp& r, const fp& a, const fp& b) {
 }
 #endif
 
+#if LCV_FP_CALL && !defined(LCV_HOSTSIM) && defined(LCV_SQR_IMPL)
+__device__ __noinline__ fp_ret fp_sqr_call(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4, uint32_t a5,
+                                           uint32_t a6, uint32_t a7, uint32_t a8, uint32_t a9, uint32_t a10,
+                                           uint32_t a11) {
+  const uint32_t a[12] = {a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11};
+  fp_ret r;
+  LCV_SQR_IMPL(r.v, a);
+  return r;
+}
+LCV_FN void fp_sqr(fp& r, const fp& a) {
+  fp_ret x = fp_sqr_call(a.v[0], a.v[1], a.v[2], a.v[3], a.v[4], a.v[5], a.v[6], a.v[7], a.v[8], a.v[9], a.v[10],
+                         a.v[11]);
+  LCV_COPY12(r.v, x.v);
+}
+#else
 LCV_FN void fp_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }
+#endif
 
 // Exponentiation by a fixed public exponent held in constant memory (wave-uniform branch).
 #define LCV_DEF_POW(fname, EXPARR, NBITS)                                  \
