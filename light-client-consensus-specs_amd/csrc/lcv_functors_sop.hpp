@@ -12,10 +12,13 @@
 
 enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
 
+// Every SOP functor pads its per-item LDS pitch to an odd word count: the teams of a wave then start
+// on different LDS banks (tools: a bank model of the programs gives 1.3-1.4x the conflict-free LDS
+// cycles instead of 2.7-3.4x with the 12 * slots pitch, which is a multiple of 32 words or 16 off one)
 struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
-  static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12,
+  static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
   LCV_HD uint32_t upd(uint32_t t) const { return mode == 0 ? t >> 1 : t; }
@@ -85,7 +88,7 @@ struct F_sop_lines {
 
 struct F_sop_acc {
   Work W; SopView P;
-  static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12,
+  static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
   LCV_HD const uint32_t* io_in(uint32_t i) const { return W.lines + (size_t)i * SOP_LINE_WORDS; }
@@ -107,7 +110,7 @@ struct F_sop_acc {
 
 struct F_sop_fexp {
   Work W; SopView P;
-  static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12,
+  static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
   static_assert(LCV_SOP_FEXP_SLOT_R5_1 == LCV_SOP_FEXP_SLOT_R0_0 + 11, "r in consecutive slots");
@@ -144,7 +147,7 @@ struct F_sop_fexp {
 // formulas), affine H(m) -> W.qh and its identity flag -> W.qh_inf
 struct F_sop_h2c {
   Work W; SopView P;
-  static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12,
+  static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
   static_assert(LCV_SOP_H2C_SLOT_HY1 == LCV_SOP_H2C_SLOT_HX0 + 3, "hx, hy in consecutive slots");
