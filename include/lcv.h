@@ -93,6 +93,16 @@ int lcv_init(int device, lcv_ctx** out);
 void lcv_destroy(lcv_ctx* ctx);
 const char* lcv_last_error(const lcv_ctx* ctx);
 
+/* ---- network configuration, runtime (mainnet by default): the values sync-protocol.md reads from
+ * the preset / config — SLOTS_PER_EPOCH and EPOCHS_PER_SYNC_COMMITTEE_PERIOD (periods, UPDATE_TIMEOUT),
+ * fork_epochs4 = ALTAIR, BELLATRIX, CAPELLA, DENEB _FORK_EPOCH (is_valid_light_client_header :220-240,
+ * get_lc_execution_root :186-214, compute_fork_version :461), fork_versions20 = GENESIS, ALTAIR,
+ * BELLATRIX, CAPELLA, DENEB _FORK_VERSION (5 x 4 B), domain_sync_committee4 = DOMAIN_SYNC_COMMITTEE
+ * (:462).  Fork epochs non-decreasing.  Applies to every later validate / bootstrap call on ctx.
+ * SYNC_COMMITTEE_SIZE is the mainnet preset's 512 (the packed layouts above). */
+int lcv_set_config(lcv_ctx* ctx, uint64_t slots_per_epoch, uint64_t epochs_per_sync_committee_period,
+                   const uint64_t* fork_epochs4, const uint8_t* fork_versions20, const uint8_t* domain_sync_committee4);
+
 /* ---- validate_light_client_update (sync-protocol.md:386-465) against one store snapshot.
  * The store's two committees (SSZ SyncCommittee bytes; an all-zero next committee means
  * "not known", sync-protocol.md:316-317) are decoded and KeyValidated once, device resident.

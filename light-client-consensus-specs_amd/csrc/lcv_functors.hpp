@@ -167,11 +167,11 @@ struct F_import_pq {  // debug pairing inputs: P -> W.pk, Q -> W.qh (no validati
 // 54 -> depth 5, subtree index 22, rooted at header.beacon.state_root)
 struct F_bootstrap {
   const uint8_t* beacon; const uint8_t* exec; const uint8_t* branch; const uint8_t* sc; const uint8_t* sc_branch;
-  const uint8_t* trusted; uint8_t* out;
+  const uint8_t* trusted; uint8_t* out; NetConfig cfg;
   LCV_HD void operator()(uint32_t i) const {
     const uint8_t* b = beacon + (size_t)K_BEACON * i;
     uint8_t r = 0;
-    if (!lc_header_valid(b, exec + (size_t)K_EXEC * i, branch + (size_t)K_EXEC_BRANCH * i)) {
+    if (!lc_header_valid(b, exec + (size_t)K_EXEC * i, branch + (size_t)K_EXEC_BRANCH * i, cfg)) {
       r = 1;
     } else {
       h256 root, t;

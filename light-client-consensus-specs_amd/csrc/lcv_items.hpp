@@ -40,6 +40,7 @@ struct BatchDev {
 };
 
 struct Params {
+  NetConfig cfg;
   uint64_t current_slot;
   uint64_t store_fin_slot;
   uint32_t next_known;
@@ -192,11 +193,11 @@ LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
   // :392 participants
   if (popcount_bits(B.bits + 64 * (size_t)i) < 1) LCV_FAIL(1);
   // :395 attested header
-  if (!lc_header_valid(ab, ae, abr)) LCV_FAIL(2);
+  if (!lc_header_valid(ab, ae, abr, P.cfg)) LCV_FAIL(2);
   // :398 slot ordering
   if (!(P.current_slot >= sig_slot && sig_slot > att_slot && att_slot >= fin_slot)) LCV_FAIL(3);
-  const uint64_t store_period = period_of_slot(P.store_fin_slot);
-  const uint64_t sig_period = period_of_slot(sig_slot);
+  const uint64_t store_period = period_of_slot(P.store_fin_slot, P.cfg);
+  const uint64_t sig_period = period_of_slot(sig_slot, P.cfg);
   const bool next_known = P.next_known != 0;
   if (next_known) {
     if (!(sig_period == store_period || sig_period == store_period + 1)) LCV_FAIL(4);  // :402
@@ -204,7 +205,7 @@ LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
     if (sig_period != store_period) LCV_FAIL(5);  // :404
   }
   // :407-414 relevance
-  const uint64_t att_period = period_of_slot(att_slot);
+  const uint64_t att_period = period_of_slot(att_slot, P.cfg);
   const bool is_sc = !bytes_all_zero(nbr, K_NSC_BRANCH / 4);
   const bool has_next = !next_known && is_sc && att_period == store_period;
   if (!(att_slot > P.store_fin_slot || has_next)) LCV_FAIL(6);
@@ -222,7 +223,7 @@ LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
       if (!fin_default) LCV_FAIL(8);
       h256_zero(leaf);
     } else {
-      if (!lc_header_valid(fb, fe, fbr)) LCV_FAIL(9);
+      if (!lc_header_valid(fb, fe, fbr, P.cfg)) LCV_FAIL(9);
       htr_beacon(leaf, fb);
     }
     if (!merkle_branch_ok(leaf, finb, 6, 41, state_root)) LCV_FAIL(10);
@@ -242,7 +243,7 @@ LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
   W.comm_id[i] = sig_period != store_period ? 1u : 0u;
   h256 gvr, msg;
   LCV_UNROLL for (int k = 0; k < 8; ++k) gvr.w[k] = P.gvr[k];
-  signing_root(msg, ab, sig_slot, gvr);
+  signing_root(msg, ab, sig_slot, gvr, P.cfg);
   soa_st_h256(W.msg, W.cap, i, msg);
   W.pre_reason[i] = (uint8_t)reason;
 }

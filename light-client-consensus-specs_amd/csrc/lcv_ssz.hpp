@@ -22,14 +22,38 @@ enum {
   K_SC = 24624,
 };
 
-constexpr uint64_t LCV_SLOTS_PER_EPOCH = 32;
-constexpr uint64_t LCV_EPOCHS_PER_PERIOD = 256;
-constexpr uint64_t LCV_CAPELLA_EPOCH = 194048;
-constexpr uint64_t LCV_DENEB_EPOCH = 269568;
-constexpr uint64_t LCV_BELLATRIX_EPOCH = 144896;
-constexpr uint64_t LCV_ALTAIR_EPOCH = 74240;
+// The network configuration the light-client path reads (lcv_set_config; mainnet by default): the
+// preset's SLOTS_PER_EPOCH and EPOCHS_PER_SYNC_COMMITTEE_PERIOD (UPDATE_TIMEOUT's factors,
+// compute_sync_committee_period_at_slot), the config's fork epochs (is_valid_light_client_header
+// sync-protocol.md:220-240, get_lc_execution_root :186-214) and fork versions (compute_fork_version
+// at :461), and DOMAIN_SYNC_COMMITTEE (:462).  SYNC_COMMITTEE_SIZE stays the mainnet preset's 512
+// (the packed layouts of include/lcv.h).
+struct NetConfig {
+  uint64_t slots_per_epoch;
+  uint64_t epochs_per_period;
+  uint64_t fork_epoch[4];          // ALTAIR, BELLATRIX, CAPELLA, DENEB
+  uint32_t fork_version[5];        // GENESIS, ALTAIR, BELLATRIX, CAPELLA, DENEB (big-endian words)
+  uint32_t domain_sync_committee;  // big-endian word
+};
+enum { FORK_ALTAIR = 0, FORK_BELLATRIX = 1, FORK_CAPELLA = 2, FORK_DENEB = 3 };
 
-LCV_FN uint64_t period_of_slot(uint64_t slot) { return slot / (LCV_SLOTS_PER_EPOCH * LCV_EPOCHS_PER_PERIOD); }
+inline NetConfig net_config_mainnet() {
+  NetConfig c;
+  c.slots_per_epoch = 32;
+  c.epochs_per_period = 256;
+  c.fork_epoch[FORK_ALTAIR] = 74240;
+  c.fork_epoch[FORK_BELLATRIX] = 144896;
+  c.fork_epoch[FORK_CAPELLA] = 194048;
+  c.fork_epoch[FORK_DENEB] = 269568;
+  for (uint32_t k = 0; k < 5; ++k) c.fork_version[k] = k << 24;  // 0x0k000000
+  c.domain_sync_committee = 0x07000000u;
+  return c;
+}
+
+LCV_FN uint64_t epoch_of_slot(uint64_t slot, const NetConfig& c) { return slot / c.slots_per_epoch; }
+LCV_FN uint64_t period_of_slot(uint64_t slot, const NetConfig& c) {
+  return slot / (c.slots_per_epoch * c.epochs_per_period);
+}
 
 // hash_tree_root(BeaconBlockHeader): 5 leaves -> 8, 6 hashes
 LCV_FN void htr_beacon(h256& root, const uint8_t* b) {
@@ -115,15 +139,15 @@ LCV_FN void htr_exec(h256& root, const uint8_t* rec, bool deneb) {
 }
 
 // is_valid_light_client_header (sync-protocol.md:220-240)
-LCV_FN bool lc_header_valid(const uint8_t* beacon, const uint8_t* exec, const uint8_t* branch) {
-  const uint64_t epoch = ld_le64(beacon) / LCV_SLOTS_PER_EPOCH;
+LCV_FN bool lc_header_valid(const uint8_t* beacon, const uint8_t* exec, const uint8_t* branch, const NetConfig& cfg) {
+  const uint64_t epoch = epoch_of_slot(ld_le64(beacon), cfg);
   const uint64_t blob = ld_le64(exec + 32 * 15);
   const uint64_t excess = ld_le64(exec + 32 * 16);
-  if (epoch < LCV_DENEB_EPOCH && (blob | excess) != 0) return false;
-  if (epoch < LCV_CAPELLA_EPOCH)
+  if (epoch < cfg.fork_epoch[FORK_DENEB] && (blob | excess) != 0) return false;
+  if (epoch < cfg.fork_epoch[FORK_CAPELLA])
     return bytes_all_zero(exec, K_EXEC / 4) && bytes_all_zero(branch, K_EXEC_BRANCH / 4);
   h256 root, body;
-  htr_exec(root, exec, epoch >= LCV_DENEB_EPOCH);
+  htr_exec(root, exec, epoch >= cfg.fork_epoch[FORK_DENEB]);
   ld_chunk(body, beacon + 80);
   return merkle_branch_ok(root, branch, 4, 9, body);
 }
@@ -162,22 +186,24 @@ LCV_FN void htr_sync_committee(h256& root, const uint8_t* sc) {
   hash_pair(root, s[9], agg);
 }
 
-LCV_FN void fork_version_word(uint32_t& v, uint64_t epoch) {
-  if (epoch >= LCV_DENEB_EPOCH) v = 0x04000000u;
-  else if (epoch >= LCV_CAPELLA_EPOCH) v = 0x03000000u;
-  else if (epoch >= LCV_BELLATRIX_EPOCH) v = 0x02000000u;
-  else if (epoch >= LCV_ALTAIR_EPOCH) v = 0x01000000u;
-  else v = 0;
+// compute_fork_version (its fork cascade, sync-protocol.md:461)
+LCV_FN uint32_t fork_version_word(uint64_t epoch, const NetConfig& c) {
+  uint32_t v = c.fork_version[0];
+  LCV_UNROLL for (int k = 0; k < 4; ++k)
+    if (epoch >= c.fork_epoch[k]) v = c.fork_version[k + 1];
+  return v;
 }
 
 // compute_signing_root(attested.beacon, compute_domain(DOMAIN_SYNC_COMMITTEE, fork_version, gvr))
-LCV_FN void signing_root(h256& out, const uint8_t* att_beacon, uint64_t signature_slot, const h256& gvr) {
+// (sync-protocol.md:460-463)
+LCV_FN void signing_root(h256& out, const uint8_t* att_beacon, uint64_t signature_slot, const h256& gvr,
+                         const NetConfig& cfg) {
   const uint64_t fslot = (signature_slot > 1 ? signature_slot : 1) - 1;
   h256 ver, fdr, dom, obj;
   h256_zero(ver);
-  fork_version_word(ver.w[0], fslot / LCV_SLOTS_PER_EPOCH);
+  ver.w[0] = fork_version_word(epoch_of_slot(fslot, cfg), cfg);
   hash_pair(fdr, ver, gvr);
-  dom.w[0] = 0x07000000u;  // DOMAIN_SYNC_COMMITTEE
+  dom.w[0] = cfg.domain_sync_committee;
   LCV_UNROLL for (int i = 1; i < 8; ++i) dom.w[i] = fdr.w[i - 1];
   htr_beacon(obj, att_beacon);
   hash_pair(out, obj, dom);

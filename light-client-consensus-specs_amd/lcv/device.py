@@ -7,6 +7,7 @@ from typing import Dict, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import config as _config
 from ._native import Lib, LcvError, UpdateBatch, HeaderCols, as_u8, load, ptr
 
 SYNC_COMMITTEE_BYTES = 24624
@@ -110,6 +111,7 @@ class Verifier:
         if rc != 0:
             raise LcvError(f"lcv_init(device={device}) failed with status {rc}")
         self.device = device
+        self.config = _config.MAINNET  # the context's network configuration (lcv_init: mainnet)
 
     # ------------------------------------------------------------------ plumbing
     def _check(self, rc: int, what: str):
@@ -127,6 +129,15 @@ class Verifier:
             self.close()
         except Exception:
             pass
+
+    def set_config(self, cfg: "_config.NetworkConfig") -> None:
+        """The network configuration this context validates under (lcv_set_config; mainnet after init)."""
+        epochs = np.array(cfg.fork_epochs(), np.uint64)
+        versions = np.frombuffer(b"".join(cfg.fork_versions()), np.uint8).copy()
+        dom = np.frombuffer(cfg.DOMAIN_SYNC_COMMITTEE, np.uint8).copy()
+        self._check(self.lib.lcv_set_config(self.ctx, int(cfg.SLOTS_PER_EPOCH), int(cfg.EPOCHS_PER_SYNC_COMMITTEE_PERIOD),
+                                            ptr(epochs, C.c_uint64), ptr(versions), ptr(dom)), "lcv_set_config")
+        self.config = cfg
 
     def set_pipeline(self, streams: int, chunks: int) -> None:
         """Run validate's per-update stage chain on `chunks` slices over `streams` HIP streams

@@ -12,6 +12,7 @@ import hashlib
 import threading
 from typing import Dict, Optional
 
+from . import config
 from .device import Verifier
 
 _lock = threading.Lock()
@@ -34,11 +35,19 @@ def set_default_verifier(v: Optional[Verifier]) -> None:
 
 
 def default_verifier() -> Verifier:
+    """The process-wide context (opened on first use, with the active network configuration)."""
     global _default
     with _lock:
         if _default is None:
-            _default = Verifier(_device)
+            v = Verifier(_device)
+            if config.active() != config.MAINNET:
+                v.set_config(config.active())
+            _default = v
         return _default
+
+
+def current_default() -> Optional[Verifier]:
+    return _default
 
 
 def ensure_store(v: Verifier, finalized_slot: int, current: bytes, nxt: bytes) -> None:

@@ -32,13 +32,14 @@ from typing import Any, Optional, Sequence
 
 import numpy as np
 
+from . import config
 from . import layout as L
 from . import runtime
 from .device import Verifier
 from .sync_protocol import REASONS, validate_light_client_updates
 
-SLOTS_PER_PERIOD = 32 * 256  # SLOTS_PER_EPOCH * EPOCHS_PER_SYNC_COMMITTEE_PERIOD (mainnet)
-UPDATE_TIMEOUT = SLOTS_PER_PERIOD  # sync-protocol.md:89
+# SLOTS_PER_EPOCH * EPOCHS_PER_SYNC_COMMITTEE_PERIOD and UPDATE_TIMEOUT (sync-protocol.md:89) come from the
+# active network configuration (lcv.config.active(); mainnet unless set)
 
 
 # ------------------------------------------------------------------ predicates (sync-protocol.md:246-341)
@@ -47,7 +48,7 @@ def _zero(b: bytes) -> bool:
 
 
 def compute_sync_committee_period_at_slot(slot) -> int:
-    return int(slot) // SLOTS_PER_PERIOD
+    return config.active().compute_sync_committee_period_at_slot(slot)
 
 
 def is_sync_committee_update(update) -> bool:
@@ -129,7 +130,7 @@ def apply_light_client_update(store, update) -> None:
 def process_light_client_store_force_update(store, current_slot: int) -> None:
     """sync-protocol.md:490-503 (the best update's finalized header is replaced on a copy, so the
     caller's update object is not mutated)."""
-    if int(current_slot) > _slot(store.finalized_header) + UPDATE_TIMEOUT and store.best_valid_update is not None:
+    if int(current_slot) > _slot(store.finalized_header) + config.active().UPDATE_TIMEOUT and store.best_valid_update is not None:
         best = store.best_valid_update
         if _slot(best.finalized_header) <= _slot(store.finalized_header):
             best = SimpleNamespace(**{k: getattr(best, k) for k in _UPDATE_FIELDS})

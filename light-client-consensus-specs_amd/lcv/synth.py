@@ -25,18 +25,13 @@ from typing import Optional
 
 import numpy as np
 
+from . import config as _config
 from . import layout as L
+from .config import NetworkConfig
 from .device import PackedUpdates, Verifier
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-SLOTS_PER_EPOCH = 32
-SLOTS_PER_PERIOD = 32 * 256
-CAPELLA_FORK_EPOCH = 194048
-DENEB_FORK_EPOCH = 269568
-DOMAIN_SYNC_COMMITTEE = bytes.fromhex("07000000")
-FORK_VERSIONS = ((269568, bytes.fromhex("04000000")), (194048, bytes.fromhex("03000000")),
-                 (144896, bytes.fromhex("02000000")), (74240, bytes.fromhex("01000000")),
-                 (0, bytes.fromhex("00000000")))
+# network values come from a NetworkConfig (lcv.config; the active one unless given)
 DENEB_PERIOD = 1100    # slot 9,011,200: a Deneb-era sync-committee period
 CAPELLA_PERIOD = 1000  # slot 8,192,000: a Capella-era period
 
@@ -115,17 +110,13 @@ def htr_sync_committee(sc: bytes) -> bytes:
     return sha256(merkleize(roots, 9) + htr_pubkey(sc[512 * 48:]))
 
 
-def fork_version(epoch: int) -> bytes:
-    for e, v in FORK_VERSIONS:
-        if epoch >= e:
-            return v
-    return FORK_VERSIONS[-1][1]
-
-
-def signing_root(att_beacon: bytes, signature_slot: int, gvr: bytes) -> bytes:
+def signing_root(att_beacon: bytes, signature_slot: int, gvr: bytes, cfg: Optional[NetworkConfig] = None) -> bytes:
+    """compute_signing_root(attested beacon, compute_domain(DOMAIN_SYNC_COMMITTEE, fork_version, gvr))
+    (sync-protocol.md:460-463) under `cfg` (the active configuration by default)."""
+    cfg = cfg or _config.active()
     fslot = max(int(signature_slot), 1) - 1
-    fdr = sha256(fork_version(fslot // SLOTS_PER_EPOCH) + bytes(28) + gvr)
-    domain = DOMAIN_SYNC_COMMITTEE + fdr[:28]
+    fdr = sha256(cfg.compute_fork_version(cfg.compute_epoch_at_slot(fslot)) + bytes(28) + gvr)
+    domain = cfg.DOMAIN_SYNC_COMMITTEE + fdr[:28]
     return sha256(htr_beacon(att_beacon) + domain)
 
 
@@ -190,13 +181,13 @@ def _rand_exec(rng: np.random.Generator, deneb: bool) -> bytes:
     return bytes(rec)
 
 
-def _header(rng, slot: int):
+def _header(rng, slot: int, cfg: NetworkConfig):
     """Random LightClientHeader at `slot` with a valid execution branch (body root derived); before
     Capella the execution header and branch are empty (as upgraded Altair headers are)."""
-    epoch = slot // SLOTS_PER_EPOCH
-    if epoch < CAPELLA_FORK_EPOCH:
+    epoch = cfg.compute_epoch_at_slot(slot)
+    if epoch < cfg.CAPELLA_FORK_EPOCH:
         return slot, bytes(L.EXEC_BYTES), bytes(128), rng.bytes(32)
-    deneb = epoch >= DENEB_FORK_EPOCH
+    deneb = epoch >= cfg.DENEB_FORK_EPOCH
     ex = _rand_exec(rng, deneb)
     br = [rng.bytes(32) for _ in range(4)]
     body = fold_branch(htr_exec_record(ex, deneb), br, 9)
@@ -205,14 +196,18 @@ def _header(rng, slot: int):
 
 def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERIOD, participation: str = "full",
              kinds: Optional[np.ndarray] = None, with_next: bool = True, with_finality: bool = True,
-             committees=None, gvr: Optional[bytes] = None, sign_next: bool = False, npool: int = 1) -> SyntheticBatch:
+             committees=None, gvr: Optional[bytes] = None, sign_next: bool = False, npool: int = 1,
+             cfg: Optional[NetworkConfig] = None) -> SyntheticBatch:
     """n synthetic updates against one store (finalized at the first slot of `period`, both
     committees known).  participation: "full" (512/512) or "random" (popcount uniform in [342,512]).
     kinds: optional per-row corruption kinds (see K_*).  sign_next: signature slots in the next period,
     signed by the next committee (sync-protocol.md:452-455 selects it).  npool > 1 (BASELINE configs[3],
     the SHA-256-heavy form): update i carries next_sync_committee number i % npool out of npool
     distinct committees (HTR(SyncCommittee), 1,025 SHA-256 calls, then runs once per distinct value);
-    the store's next committee is then unknown, as :441-442 would otherwise demand equality with it."""
+    the store's next committee is then unknown, as :441-442 would otherwise demand equality with it.
+    cfg: the network configuration the rows are built and signed under (default: lcv.config.active())."""
+    cfg = cfg or _config.active()
+    SLOTS_PER_PERIOD = cfg.SLOTS_PER_PERIOD
     rng = np.random.default_rng(seed)
     cur, nxt = committees if committees is not None else (make_committee(verifier, 0), make_committee(verifier, 1))
     gvr = gvr if gvr is not None else sha256(b"lcv-synthetic-genesis-validators-root")
@@ -244,10 +239,10 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
         if sign_next:
             ss = store_fin + SLOTS_PER_PERIOD + int(rng.integers(0, 64))
         fin_slot = store_fin + int(rng.integers(0, att_slot - store_fin - 32)) if with_finality else 0
-        a_slot, a_ex, a_br, a_body = _header(rng, att_slot)
+        a_slot, a_ex, a_br, a_body = _header(rng, att_slot, cfg)
         # sparse state tree (see module docstring)
         if with_finality:
-            f_slot, f_ex, f_br, f_body = _header(rng, fin_slot)
+            f_slot, f_ex, f_br, f_body = _header(rng, fin_slot, cfg)
             f_beacon = (f_slot.to_bytes(8, "little") + int(rng.integers(0, 2 ** 20)).to_bytes(8, "little")
                         + rng.bytes(32) + rng.bytes(32) + f_body)
             fin_leaf = htr_beacon(f_beacon)
@@ -286,7 +281,7 @@ def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERI
             sks = total_sk
         else:
             sks = (total_sk - sum(signer.sks[j] for j in np.flatnonzero(bits == 0))) % R_ORDER
-        m = signing_root(a_beacon, ss, gvr)
+        m = signing_root(a_beacon, ss, gvr, cfg)
         if kind == K_BAD_SIG_MESSAGE:
             m = sha256(b"not-the-signing-root" + m)
         # corruptions of the byte records

@@ -42,6 +42,33 @@ DOMAIN_SYNC_COMMITTEE = bytes.fromhex("07000000")
 MIN_SYNC_COMMITTEE_PARTICIPANTS = 1
 UPDATE_TIMEOUT = SLOTS_PER_EPOCH * EPOCHS_PER_SYNC_COMMITTEE_PERIOD
 
+_CONFIG_NAMES = ("SLOTS_PER_EPOCH", "EPOCHS_PER_SYNC_COMMITTEE_PERIOD", "GENESIS_FORK_VERSION", "ALTAIR_FORK_VERSION",
+                 "BELLATRIX_FORK_VERSION", "CAPELLA_FORK_VERSION", "DENEB_FORK_VERSION", "ALTAIR_FORK_EPOCH",
+                 "BELLATRIX_FORK_EPOCH", "CAPELLA_FORK_EPOCH", "DENEB_FORK_EPOCH", "DOMAIN_SYNC_COMMITTEE")
+
+
+class use_config:
+    """Context manager: run the oracle (and reference blocks exec'd over reference_namespace(), which
+    reads these globals when it is built) under another network configuration: keyword values for the
+    names in _CONFIG_NAMES; UPDATE_TIMEOUT follows."""
+
+    def __init__(self, **values):
+        bad = set(values) - set(_CONFIG_NAMES)
+        assert not bad, bad
+        self.values = values
+
+    def __enter__(self):
+        g = globals()
+        self.saved = {k: g[k] for k in _CONFIG_NAMES + ("UPDATE_TIMEOUT",)}
+        g.update(self.values)
+        g["UPDATE_TIMEOUT"] = g["SLOTS_PER_EPOCH"] * g["EPOCHS_PER_SYNC_COMMITTEE_PERIOD"]
+        return self
+
+    def __exit__(self, *exc):
+        globals().update(self.saved)
+        return False
+
+
 # generalized indices (reference sync-protocol.md:78-81, pre-Electra values)
 FINALIZED_ROOT_GINDEX = 105
 CURRENT_SYNC_COMMITTEE_GINDEX = 54

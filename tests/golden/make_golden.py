@@ -39,6 +39,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 import helpers as H  # noqa: E402
 
 from lcv import synth  # noqa: E402
+from lcv.config import MAINNET, TESTNET  # noqa: E402
 from oracle import bls12_381 as B  # noqa: E402
 from oracle import spec as S  # noqa: E402
 
@@ -120,17 +121,18 @@ def build_cases(v):
     cur, nxt = synth.make_committee(v, 0), synth.make_committee(v, 1)
     comms = (cur, nxt)
     C = Cases()
-    P = synth.DENEB_PERIOD * synth.SLOTS_PER_PERIOD
+    SPP = MAINNET.SLOTS_PER_PERIOD
+    P = synth.DENEB_PERIOD * SPP
     # A: Deneb, next committee known; every corruption kind once (+ 2 valid)
     kinds = np.array([0, 0, 1, 2, 3, 4, 5, 6, 7])
     a = synth.generate(v, len(kinds), seed=21, participation="random", kinds=kinds, committees=comms)
     for i, k in enumerate(kinds):
         C.add(a.updates, i, f"deneb_kind{k}", P, 1, a.current_slot, 1)
     pa = a.updates
-    big = P + 4 * synth.SLOTS_PER_PERIOD
+    big = P + 4 * SPP
     # mutations of the valid row 0
     C.add(pa, 0, "slot_order_current", P, 1, int(pa.signature_slot[0]) - 1, 1)
-    C.add(pa, 0, "sig_period_skip", P, 1, big, 1, signature_slot=P + 2 * synth.SLOTS_PER_PERIOD + 5)
+    C.add(pa, 0, "sig_period_skip", P, 1, big, 1, signature_slot=P + 2 * SPP + 5)
     att_slot = int.from_bytes(pa.att_beacon[0][:8].tobytes(), "little")
     C.add(pa, 0, "not_relevant", att_slot, 1, a.current_slot, 1)
     C.add(pa, 0, "finalized_not_empty", P, 1, a.current_slot, 1, finality_branch=bytes(192))
@@ -164,7 +166,7 @@ def build_cases(v):
     C.add(d.updates, 0, "relevant_via_next_committee", att_d, 0, d.current_slot, 1)
     C.add(d.updates, 0, "not_relevant_next_known", att_d, 1, d.current_slot, 1)
     # E: Capella update (BASELINE config 1 substitute) and a Capella header carrying blob gas
-    PC = synth.CAPELLA_PERIOD * synth.SLOTS_PER_PERIOD
+    PC = synth.CAPELLA_PERIOD * SPP
     e = synth.generate(v, 1, seed=26, period=synth.CAPELLA_PERIOD, committees=comms)
     C.add(e.updates, 0, "capella_valid", PC, 1, e.current_slot, 1)
     ex = bytearray(e.updates.att_exec[0].tobytes())
@@ -172,7 +174,7 @@ def build_cases(v):
     C.add(e.updates, 0, "capella_blob_gas", PC, 1, e.current_slot, 1, att_exec=bytes(ex))
     # F: pre-Capella (Bellatrix) update: empty execution is valid, a non-empty one is not
     f = synth.generate(v, 1, seed=27, period=600, committees=comms)
-    PB = 600 * synth.SLOTS_PER_PERIOD
+    PB = 600 * SPP
     C.add(f.updates, 0, "bellatrix_valid", PB, 1, f.current_slot, 1)
     exb = bytearray(832)
     exb[0] = 7
@@ -420,12 +422,79 @@ def make_wire():
     print("wire:", len(msgs), "messages,", len(bmsgs), "bootstraps")
 
 
+# ----------------------------------------------------------------------------- non-mainnet configuration
+def _oracle_config(cfg):
+    """oracle/spec.use_config keywords for a lcv NetworkConfig."""
+    from oracle.spec import _CONFIG_NAMES
+    return {k: getattr(cfg, k) for k in _CONFIG_NAMES}
+
+
+def make_testnet_cases():
+    """lc_updates_testnet.npz: rows built and signed under a non-mainnet configuration (lcv.config.TESTNET:
+    its own fork versions and fork epochs), with the expected reason under that configuration AND under
+    mainnet, each from the reference's exec'd blocks (over oracle/spec.py switched to the configuration)
+    and the oracle restatement.  Row kinds: Deneb valid / bad signature / corrupted finality branch
+    (period 1100: Deneb on both networks, so only the signing domain differs), and a period-600 row
+    (Deneb on the testnet, Bellatrix on mainnet: is_valid_light_client_header differs too)."""
+    v = H.hostsim_verifier()
+    cur, nxt = synth.make_committee(v, 0), synth.make_committee(v, 1)
+    comms = (cur, nxt)
+    C = Cases()
+    SPP = TESTNET.SLOTS_PER_PERIOD
+    kinds = np.array([synth.K_VALID, synth.K_BAD_SIG_MESSAGE, synth.K_BAD_FINALITY_BRANCH, synth.K_LOW_PARTICIPATION])
+    a = synth.generate(v, len(kinds), seed=41, participation="random", kinds=kinds, committees=comms, cfg=TESTNET)
+    for i, k in enumerate(kinds):
+        C.add(a.updates, i, f"testnet_deneb_kind{k}", synth.DENEB_PERIOD * SPP, 1, a.current_slot, 1)
+    m = synth.generate(v, 1, seed=42, committees=comms, cfg=MAINNET)
+    C.add(m.updates, 0, "mainnet_signed_deneb", synth.DENEB_PERIOD * SPP, 1, m.current_slot, 1)
+    b = synth.generate(v, 2, seed=43, period=600, committees=comms, cfg=TESTNET)
+    C.add(b.updates, 0, "testnet_period600_deneb", 600 * SPP, 1, b.current_slot, 1)
+    C.add(b.updates, 1, "testnet_period600_no_next", 600 * SPP, 0, b.current_slot, 1)
+    gvr = a.genesis_validators_root
+    n = len(C.name)
+    pool = np.stack([np.frombuffer(x, np.uint8) for x in (cur.ssz, nxt.ssz, bytes(24624))])
+    arrays = {k: np.stack([np.frombuffer(r, np.uint8) for r in C.rows[k]]) for k in COLS}
+    from lcv.device import PackedUpdates
+    p = PackedUpdates(nsc_pool=pool, nsc_index=np.array(C.pool_row, np.uint32),
+                      signature_slot=np.array(C.sig_slot, np.uint64), **arrays)
+    expected = {}
+    for cfg in (TESTNET, MAINNET):
+        with S.use_config(**_oracle_config(cfg)):
+            ns, assert_lines = load_reference()
+            rs = []
+            for i in range(n):
+                nxt_bytes = nxt.ssz if C.next_known[i] else bytes(24624)
+                store_o = H.store_from(C.store_fin[i], cur.ssz, nxt_bytes)
+                r_oracle = H.O.validate_light_client_update(store_o, H.update_from(p, i), C.current_slot[i], gvr)
+                store_r, u_r = to_reference_objects(ns, p, i, C.store_fin[i], cur.ssz, nxt_bytes)
+                r_ref = reference_reason(ns, assert_lines, store_r, u_r, C.current_slot[i], gvr)
+                assert r_oracle == r_ref, (cfg.name, C.name[i], r_oracle, r_ref)
+                rs.append(r_ref)
+                print(f"{cfg.name:8s} {i:2d} {C.name[i]:32s} reason {r_ref}", flush=True)
+            expected[cfg.name] = rs
+    assert expected["testnet"] != expected["mainnet"]
+    cfgj = {k: (v_.hex() if isinstance(v_, bytes) else v_) for k, v_ in vars(TESTNET).items()}
+    np.savez_compressed(os.path.join(HERE, "lc_updates_testnet.npz"), **arrays, nsc_pool=pool,
+                        nsc_index=np.array(C.pool_row, np.uint32), signature_slot=np.array(C.sig_slot, np.uint64),
+                        store_finalized_slot=np.array(C.store_fin, np.uint64),
+                        store_next_known=np.array(C.next_known, np.uint8),
+                        current_slot=np.array(C.current_slot, np.uint64),
+                        expected_reason_testnet=np.array(expected["testnet"], np.uint8),
+                        expected_reason_mainnet=np.array(expected["mainnet"], np.uint8),
+                        genesis_validators_root=np.frombuffer(gvr, np.uint8))
+    json.dump({"cases": C.name, "config": cfgj, "expected_reason": expected},
+              open(os.path.join(HERE, "lc_updates_testnet.json"), "w"), indent=1)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "store":
         make_store_sequence()
+    elif len(sys.argv) > 1 and sys.argv[1] == "testnet":
+        make_testnet_cases()
     elif len(sys.argv) > 1 and sys.argv[1] == "wire":
         make_wire()
     else:
         main()
         make_store_sequence()
         make_wire()
+        make_testnet_cases()

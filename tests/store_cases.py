@@ -62,6 +62,6 @@ def run(verifier):
         assert list(acc.astype(np.uint8)) == list(z["accepted"][case])
         assert reasons == list(z["reason"][case])
         assert summary(st) == list(z["summary"][case][n - 1])
-        force = int(st.finalized_header.beacon.slot) + LS.UPDATE_TIMEOUT + 1
+        force = int(st.finalized_header.beacon.slot) + LS.config.active().UPDATE_TIMEOUT + 1
         LS.process_light_client_store_force_update(st, force)
         assert summary(st) == list(z["summary"][case][n])

@@ -12,6 +12,13 @@ def test_update_cases_gpu(gpu_verifier):
     assert list(got) == list(exp)
 
 
+def test_testnet_config_gpu(gpu_verifier):
+    """lcv_set_config on the device: non-mainnet fork versions / epochs (reference-exec'd reasons)."""
+    got_t, exp_t, got_m, exp_m = G.run_testnet_cases(gpu_verifier)
+    assert list(got_t) == list(exp_t)
+    assert list(got_m) == list(exp_m)
+
+
 def test_bls_vectors_gpu(gpu_verifier):
     b = G.load_bls()
     out, inf = gpu_verifier.debug_hash_to_g2(b["h2c_msg"])

@@ -29,3 +29,27 @@ def test_bls_vectors_hostsim(sim_verifier):
     assert sim_verifier.fast_aggregate_verify(pks, m, s)
     assert not sim_verifier.fast_aggregate_verify(pks[:2], m, s)
     assert not sim_verifier.fast_aggregate_verify(pks + [bytes([0xC0]) + bytes(47)], m, s)
+
+
+def test_testnet_config_hostsim(sim_verifier):
+    """lcv_set_config: the same rows are valid under the configuration they were signed under and
+    fail (signing domain / header fork rules) under mainnet, as the reference's exec'd blocks say."""
+    got_t, exp_t, got_m, exp_m = G.run_testnet_cases(sim_verifier)
+    assert list(got_t) == list(exp_t)
+    assert list(got_m) == list(exp_m)
+    assert list(exp_t) != list(exp_m)
+
+
+def test_config_validation(sim_verifier):
+    import pytest
+    from lcv._native import LcvError
+    from lcv.config import MAINNET, NetworkConfig
+    with pytest.raises(ValueError):
+        NetworkConfig(CAPELLA_FORK_EPOCH=10, BELLATRIX_FORK_EPOCH=20)
+    bad = MAINNET.with_(name="x")
+    object.__setattr__(bad, "DENEB_FORK_EPOCH", 5)  # bypass the dataclass check: the C ABI checks too
+    with pytest.raises(LcvError):
+        sim_verifier.set_config(bad)
+    assert MAINNET.compute_fork_version(MAINNET.DENEB_FORK_EPOCH) == bytes.fromhex("04000000")
+    assert MAINNET.compute_fork_version(MAINNET.CAPELLA_FORK_EPOCH - 1) == bytes.fromhex("02000000")
+    assert MAINNET.UPDATE_TIMEOUT == 8192
