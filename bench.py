@@ -329,15 +329,15 @@ def config_lines(v) -> dict:
                 "ms_per_pass": round(1000 * dt, 3), "verdicts_match_construction": ok,
                 "valid_fraction": round(float((sb.expected_reason == 0).mean()), 4), "stage_kernel_ms": stages}
     t0 = time.perf_counter()
-    base = synth.generate(v, 31250, seed=3, participation="random")
-    out["configs[2]"] = timed(synth.tile(base, 4), "125,000 updates (the 1M / 8-GPU batch's per-GPU shard), "
+    base = synth.generate(v, 15625, seed=3, participation="random")
+    out["configs[2]"] = timed(synth.tile(base, 8), "125,000 updates (the 1M / 8-GPU batch's per-GPU shard), "
                                                    "random participation 342..512")
     sb3 = synth.generate(v, 10000, seed=4, npool=10000)
     out["configs[3]"] = timed(sb3, "10,000 Deneb updates, all branches, a DISTINCT next_sync_committee each "
                                    "(HTR(SyncCommittee) per update)")
-    kinds = synth.adversarial_kinds(65536, seed=5, bad_fraction=0.10)
-    b4 = synth.generate(v, 65536, seed=5, participation="random", kinds=kinds)
-    out["configs[4]"] = timed(synth.tile(b4, 16), "1,048,576 adversarial updates on one GPU: 10% bad (bad "
+    kinds = synth.adversarial_kinds(16384, seed=5, bad_fraction=0.10)
+    b4 = synth.generate(v, 16384, seed=5, participation="random", kinds=kinds)
+    out["configs[4]"] = timed(synth.tile(b4, 64), "1,048,576 adversarial updates on one GPU: 10% bad (bad "
                                                   "signature message/encoding, corrupted branch, sub-2/3 "
                                                   "participation = VALID)", reps=1)
     log(f"configs[2..4] lines in {time.perf_counter() - t0:.1f}s")

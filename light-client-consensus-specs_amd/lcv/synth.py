@@ -1,32 +1,31 @@
-"""Synthetic mainnet-preset light-client updates (producer side), for the benchmark and tests.
+"""Synthetic light-client updates for the benchmark and tests, DERIVED by the producer.
 
-Follows the producer semantics of `create_light_client_update` (reference full-node.md:138-182):
-every update carries an attested header, a finalized header with its finality branch (gindex 105),
-the next sync committee with its branch (gindex 55) and Deneb execution branches (gindex 25), all
-consistent with ONE sparse BeaconState tree per update:
-
-    state root = node 1;  finality branch  = [n104, n53, n27, n12, n7, n2]   (leaf n105)
-                          next-SC branch   = [n54, n26, n12, n7, n2]          (leaf n55)
-    n27 = H(n54 = HTR(current_sync_committee), n55 = HTR(next_sync_committee))
-    body root: execution branch = [n24, n13, n7, n2] (leaf n25 = HTR(execution header))
+Every row is what a full node would serve: lcv.producer.create_light_client_update (the reference's
+full-node.md:138-188, pinned byte-for-byte against the reference's exec'd blocks in
+tests/test_producer.py) over a chain finalized block <- attested block <- signature block, each with a
+sparse random BeaconState view (every state field but the five light clients read is a random root).
+So the finality branch (gindex 105), next-sync-committee branch (gindex 55), execution branches
+(gindex 25) and signing root are all consistent with real state / block trees.
 
 The sync aggregate signature is (sum of participant secret keys) * H(signing_root), computed by the
 device signer (`Verifier.sign_batch`), so generating 10^4..10^6 validly signed updates is cheap.
-SHA-256 for the synthetic trees runs on the host (hashlib): this is input generation, outside every
-timed region, and is never the verified path.
+SHA-256 for the trees runs on the host (hashlib): this is input generation, outside every timed
+region, and is never the verified path.
 
 Corruption kinds (BASELINE.json config 5): each row has a `kind`; the expected verdict follows.
 """
 from __future__ import annotations
 
 import hashlib
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from typing import Optional
 
 import numpy as np
 
 from . import config as _config
 from . import layout as L
+from . import producer as PR
+from .producer import fold_branch, htr_beacon, htr_exec_record, htr_pubkey, htr_sync_committee, merkleize  # noqa: F401
 from .config import NetworkConfig
 from .device import PackedUpdates, Verifier
 
@@ -50,64 +49,6 @@ EXPECTED_REASON = {K_VALID: 0, K_LOW_PARTICIPATION: 0, K_BAD_SIG_MESSAGE: 14, K_
 
 def sha256(b: bytes) -> bytes:
     return hashlib.sha256(b).digest()
-
-
-def _zero_hashes(n: int = 8):
-    z = [bytes(32)]
-    for _ in range(n):
-        z.append(sha256(z[-1] + z[-1]))
-    return z
-
-
-ZH = _zero_hashes()
-
-
-def merkleize(chunks, depth: int) -> bytes:
-    layer = list(chunks)
-    for d in range(depth):
-        if len(layer) % 2:
-            layer.append(ZH[d])
-        layer = [sha256(layer[i] + layer[i + 1]) for i in range(0, len(layer), 2)]
-    return layer[0]
-
-
-def htr_beacon(b112: bytes) -> bytes:
-    chunks = [b112[0:8] + bytes(24), b112[8:16] + bytes(24), b112[16:48], b112[48:80], b112[80:112]]
-    return merkleize(chunks, 3)
-
-
-def htr_exec_record(rec: bytes, deneb: bool) -> bytes:
-    """hash_tree_root of the ExecutionPayloadHeader held in an 832-byte execution record."""
-    bloom = rec[L.EXEC_BLOOM_OFF:L.EXEC_BLOOM_OFF + 256]
-    bloom_root = merkleize([bloom[32 * k:32 * k + 32] for k in range(8)], 3)
-    ext_len = int.from_bytes(rec[L.EXEC_EXTRALEN_OFF:L.EXEC_EXTRALEN_OFF + 4], "little")
-    extra_root = sha256(rec[320:352] + ext_len.to_bytes(8, "little") + bytes(24))
-    nf = 17 if deneb else 15
-    leaves = []
-    for k in range(nf):
-        if k == 4:
-            leaves.append(bloom_root)
-        elif k == 10:
-            leaves.append(extra_root)
-        else:
-            leaves.append(rec[32 * k:32 * k + 32])
-    return merkleize(leaves, 5 if deneb else 4)
-
-
-def fold_branch(leaf: bytes, branch, index: int) -> bytes:
-    v = leaf
-    for i, b in enumerate(branch):
-        v = sha256(b + v) if (index >> i) & 1 else sha256(v + b)
-    return v
-
-
-def htr_pubkey(pk: bytes) -> bytes:
-    return sha256(pk[:32] + pk[32:48] + bytes(16))
-
-
-def htr_sync_committee(sc: bytes) -> bytes:
-    roots = [htr_pubkey(sc[48 * j:48 * j + 48]) for j in range(512)]
-    return sha256(merkleize(roots, 9) + htr_pubkey(sc[512 * 48:]))
 
 
 def signing_root(att_beacon: bytes, signature_slot: int, gvr: bytes, cfg: Optional[NetworkConfig] = None) -> bytes:
@@ -164,20 +105,29 @@ class SyntheticBatch:
 
 
 def _rand_exec(rng: np.random.Generator, deneb: bool) -> bytes:
+    """A random execution record (include/lcv.h layout) from one draw of random bytes."""
+    r = rng.bytes(7 * 32 + 20 + 4 * 8 + 1 + 32 + 8 + 256 + 16)
     rec = bytearray(L.EXEC_BYTES)
-    for k in (0, 2, 3, 5, 12, 13, 14):
-        rec[32 * k:32 * k + 32] = rng.bytes(32)
-    rec[32:52] = rng.bytes(20)                                              # fee_recipient
-    for k in (6, 7, 8, 9):
-        rec[32 * k:32 * k + 8] = int(rng.integers(0, 2 ** 62)).to_bytes(8, "little")
-    elen = int(rng.integers(0, 33))
-    rec[320:320 + elen] = rng.bytes(elen)                                   # extra_data
+    for j, k in enumerate((0, 2, 3, 5, 12, 13, 14)):
+        rec[32 * k:32 * k + 32] = r[32 * j:32 * j + 32]
+    o = 224
+    rec[32:52] = r[o:o + 20]                                                 # fee_recipient
+    o += 20
+    for k in (6, 7, 8, 9):                                                   # u64 fields (< 2^62)
+        rec[32 * k:32 * k + 8] = r[o:o + 7] + bytes([r[o + 7] & 0x3F])
+        o += 8
+    elen = r[o] % 33
+    o += 1
+    rec[320:320 + elen] = r[o:o + elen]                                      # extra_data
+    o += 32
     rec[L.EXEC_EXTRALEN_OFF:L.EXEC_EXTRALEN_OFF + 4] = elen.to_bytes(4, "little")
-    rec[352:352 + 32] = int(rng.integers(0, 2 ** 62)).to_bytes(32, "little")  # base_fee_per_gas
-    rec[L.EXEC_BLOOM_OFF:L.EXEC_BLOOM_OFF + 256] = rng.bytes(256)
-    if deneb:
-        rec[480:488] = int(rng.integers(0, 2 ** 20)).to_bytes(8, "little")
-        rec[512:520] = int(rng.integers(0, 2 ** 20)).to_bytes(8, "little")
+    rec[352:352 + 8] = r[o:o + 7] + bytes([r[o + 7] & 0x3F])                 # base_fee_per_gas
+    o += 8
+    rec[L.EXEC_BLOOM_OFF:L.EXEC_BLOOM_OFF + 256] = r[o:o + 256]
+    o += 256
+    if deneb:                                                                # blob gas (< 2^20)
+        rec[480:483] = r[o:o + 2] + bytes([r[o + 2] & 0x0F])
+        rec[512:515] = r[o + 8:o + 10] + bytes([r[o + 10] & 0x0F])
     return bytes(rec)
 
 
@@ -194,132 +144,145 @@ def _header(rng, slot: int, cfg: NetworkConfig):
     return slot, ex, b"".join(br), body
 
 
+def _rand_body_roots(rng) -> np.ndarray:
+    return np.frombuffer(rng.bytes(32 * PR.BODY_FIELDS), np.uint8).reshape(PR.BODY_FIELDS, 32)
+
+
+def _rand_state_roots(rng) -> np.ndarray:
+    return np.frombuffer(rng.bytes(32 * PR.STATE_FIELDS), np.uint8).reshape(PR.STATE_FIELDS, 32)
+
+
+def _block(rng, slot: int, cfg: NetworkConfig, parent_root: Optional[bytes] = None, bits: bytes = b"\xff" * 64,
+           sig: bytes = bytes(96), payload: bool = True) -> PR.BeaconBlockView:
+    """A block view at `slot` with random body contents (an execution payload from Capella on; a block
+    whose light-client header is never taken, payload=False, keeps its payload by root only)."""
+    epoch = cfg.compute_epoch_at_slot(slot)
+    ex = _rand_exec(rng, epoch >= cfg.DENEB_FORK_EPOCH) if payload and epoch >= cfg.CAPELLA_FORK_EPOCH else None
+    return PR.BeaconBlockView(slot=slot, proposer_index=int(rng.integers(0, 2 ** 20)),
+                              parent_root=parent_root if parent_root is not None else rng.bytes(32),
+                              state_root=bytes(32), sync_committee_bits=bits, sync_committee_signature=sig,
+                              execution=ex, execution_deneb=epoch >= cfg.DENEB_FORK_EPOCH,
+                              body_roots=_rand_body_roots(rng))
+
+
+def _with_state(rng, blk: PR.BeaconBlockView, fin_epoch: int, fin_root: bytes, cur: bytes, nxt: bytes):
+    """(post-state view, block view with its state_root) for `blk`: the state's latest_block_header is
+    the block's header with a zero state_root (as a state holds it)."""
+    hdr = blk.header()
+    st = PR.BeaconStateView(slot=blk.slot, latest_block_header=hdr[:48] + bytes(32) + hdr[80:],
+                            finalized_checkpoint_epoch=fin_epoch, finalized_checkpoint_root=fin_root,
+                            current_sync_committee=cur, next_sync_committee=nxt, field_roots=_rand_state_roots(rng))
+    return st, replace(blk, state_root=st.hash_tree_root())
+
+
 def generate(verifier: Verifier, n: int, seed: int = 2, period: int = DENEB_PERIOD, participation: str = "full",
              kinds: Optional[np.ndarray] = None, with_next: bool = True, with_finality: bool = True,
              committees=None, gvr: Optional[bytes] = None, sign_next: bool = False, npool: int = 1,
              cfg: Optional[NetworkConfig] = None) -> SyntheticBatch:
     """n synthetic updates against one store (finalized at the first slot of `period`, both
-    committees known).  participation: "full" (512/512) or "random" (popcount uniform in [342,512]).
-    kinds: optional per-row corruption kinds (see K_*).  sign_next: signature slots in the next period,
-    signed by the next committee (sync-protocol.md:452-455 selects it).  npool > 1 (BASELINE configs[3],
-    the SHA-256-heavy form): update i carries next_sync_committee number i % npool out of npool
-    distinct committees (HTR(SyncCommittee), 1,025 SHA-256 calls, then runs once per distinct value);
-    the store's next committee is then unknown, as :441-442 would otherwise demand equality with it.
+    committees known), each DERIVED by the producer (lcv.producer.create_light_client_update, the
+    reference's full-node.md:138-188) from a chain finalized block <- ... attested block <- signature
+    block with sparse random states.  participation: "full" (512/512) or "random" (popcount uniform in
+    [342,512]).  kinds: optional per-row corruption kinds (see K_*), applied to the derived rows.
+    sign_next: signature slots in the next period, signed by the next committee (sync-protocol.md:452-455
+    selects it; the producer then leaves out next_sync_committee, full-node.md:165-168).  with_next=False
+    clears the next-committee fields of same-period rows (a provider that omits them); with_finality=False
+    derives without a finalized block.  npool > 1 (BASELINE configs[3], the SHA-256-heavy form): update i
+    carries next_sync_committee number i % npool out of npool distinct committees (HTR(SyncCommittee),
+    1,025 SHA-256 calls, then runs once per distinct value); the store's next committee is then unknown,
+    as :441-442 would otherwise demand equality with it.
     cfg: the network configuration the rows are built and signed under (default: lcv.config.active())."""
     cfg = cfg or _config.active()
-    SLOTS_PER_PERIOD = cfg.SLOTS_PER_PERIOD
+    spp, spe = cfg.SLOTS_PER_PERIOD, cfg.SLOTS_PER_EPOCH
     rng = np.random.default_rng(seed)
     cur, nxt = committees if committees is not None else (make_committee(verifier, 0), make_committee(verifier, 1))
     gvr = gvr if gvr is not None else sha256(b"lcv-synthetic-genesis-validators-root")
     kinds = np.zeros(n, np.int64) if kinds is None else np.asarray(kinds, np.int64)
-    store_fin = period * SLOTS_PER_PERIOD
+    store_fin = period * spp
     if npool > 1:
         if sign_next:
             raise ValueError("npool > 1 needs the store's next committee unknown (no next-period signing)")
         prng = np.random.default_rng(seed + 1000)
         pool_bytes = prng.integers(0, 256, (npool, L.SYNC_COMMITTEE_BYTES), dtype=np.uint8)
-        pool_roots = [bytes(r) for r in verifier.htr_sync_committee_batch(pool_bytes)]
+        for k, r in enumerate(verifier.htr_sync_committee_batch(pool_bytes)):  # device HTR, seeds the memo
+            PR._SC_ROOTS[sha256(pool_bytes[k].tobytes())] = bytes(r)
         store_next = Committee([], bytes(512 * 48), bytes(48))  # is_next_sync_committee_known: False
-    nsc_root = htr_sync_committee(nxt.ssz)
-    cur_root = htr_sync_committee(cur.ssz)
     signer = nxt if sign_next else cur
     total_sk = sum(signer.sks) % R_ORDER
 
-    cols = {k: np.zeros((n, w), np.uint8) for k, w in (("att_beacon", 112), ("att_exec", 832), ("att_branch", 128),
-                                                       ("fin_beacon", 112), ("fin_exec", 832), ("fin_branch", 128),
-                                                       ("nsc_branch", 160), ("finality_branch", 192),
-                                                       ("sync_bits", 64), ("sync_signature", 96))}
-    sig_slot = np.zeros(n, np.uint64)
-    msgs = bytearray(32 * n)
-    sk_sums = bytearray(32 * n)
+    # pass 1: finalized and attested blocks + states, the participation and the message to sign
+    pending, msgs, sk_sums, bitss = [], bytearray(32 * n), bytearray(32 * n), []
     for i in range(n):
         kind = int(kinds[i])
-        att_slot = store_fin + 64 + int(rng.integers(0, SLOTS_PER_PERIOD - 256))
+        att_slot = store_fin + 64 + int(rng.integers(0, spp - 256))
         ss = att_slot + 1 + int(rng.integers(0, 64))
         if sign_next:
-            ss = store_fin + SLOTS_PER_PERIOD + int(rng.integers(0, 64))
-        fin_slot = store_fin + int(rng.integers(0, att_slot - store_fin - 32)) if with_finality else 0
-        a_slot, a_ex, a_br, a_body = _header(rng, att_slot, cfg)
-        # sparse state tree (see module docstring)
+            ss = store_fin + spp + int(rng.integers(0, 64))
+        fin_blk = None
         if with_finality:
-            f_slot, f_ex, f_br, f_body = _header(rng, fin_slot, cfg)
-            f_beacon = (f_slot.to_bytes(8, "little") + int(rng.integers(0, 2 ** 20)).to_bytes(8, "little")
-                        + rng.bytes(32) + rng.bytes(32) + f_body)
-            fin_leaf = htr_beacon(f_beacon)
+            fin_slot = store_fin + int(rng.integers(0, att_slot - store_fin - 32))
+            fin_blk = _block(rng, fin_slot, cfg)
+            fin_epoch, fin_root = fin_slot // spe, fin_blk.hash_tree_root()
         else:
-            f_ex, f_br, f_beacon, fin_leaf = bytes(832), bytes(128), bytes(112), None
-        n104, n53, n12, n7, n2 = (rng.bytes(32) for _ in range(5))
-        n55 = (pool_roots[i % npool] if npool > 1 else nsc_root) if with_next else rng.bytes(32)
-        n27 = sha256(cur_root + n55)
-        if with_finality:
-            n52 = sha256(n104 + fin_leaf)
-        else:
-            n52 = rng.bytes(32)
-        n26 = sha256(n52 + n53)
-        n13 = sha256(n26 + n27)
-        n6 = sha256(n12 + n13)
-        n3 = sha256(n6 + n7)
-        state_root = sha256(n2 + n3)
-        a_beacon = (a_slot.to_bytes(8, "little") + int(rng.integers(0, 2 ** 20)).to_bytes(8, "little")
-                    + rng.bytes(32) + state_root + a_body)
-        fin_branch = n104 + n53 + n27 + n12 + n7 + n2 if with_finality else bytes(192)
-        nsc_branch = cur_root + n26 + n12 + n7 + n2 if with_next else bytes(160)
-        # participation
+            fin_epoch, fin_root = int(rng.integers(0, store_fin // spe)), rng.bytes(32)
+        nsc = pool_bytes[i % npool].tobytes() if npool > 1 else nxt.ssz
+        att_state, att_blk = _with_state(rng, _block(rng, att_slot, cfg), fin_epoch, fin_root, cur.ssz, nsc)
         if kind == K_NO_PARTICIPANTS:
             bits = np.zeros(512, np.uint8)
         elif kind == K_LOW_PARTICIPATION:
-            pc = int(rng.integers(1, 342))
             bits = np.zeros(512, np.uint8)
-            bits[rng.choice(512, pc, replace=False)] = 1
+            bits[rng.choice(512, int(rng.integers(1, 342)), replace=False)] = 1
         elif participation == "random":
-            pc = int(rng.integers(342, 513))
             bits = np.zeros(512, np.uint8)
-            bits[rng.choice(512, pc, replace=False)] = 1
+            bits[rng.choice(512, int(rng.integers(342, 513)), replace=False)] = 1
         else:
             bits = np.ones(512, np.uint8)
-        if bits.all():
-            sks = total_sk
-        else:
-            sks = (total_sk - sum(signer.sks[j] for j in np.flatnonzero(bits == 0))) % R_ORDER
-        m = signing_root(a_beacon, ss, gvr, cfg)
+        sks = total_sk if bits.all() else (total_sk - sum(signer.sks[j] for j in np.flatnonzero(bits == 0))) % R_ORDER
+        m = signing_root(att_blk.header(), ss, gvr, cfg)
         if kind == K_BAD_SIG_MESSAGE:
             m = sha256(b"not-the-signing-root" + m)
-        # corruptions of the byte records
-        if kind == K_BAD_FINALITY_BRANCH and with_finality:
-            j = int(rng.integers(0, 192))
-            fin_branch = fin_branch[:j] + bytes([fin_branch[j] ^ 0x01]) + fin_branch[j + 1:]
-        if kind == K_BAD_NSC_BRANCH and with_next:
-            j = int(rng.integers(0, 160))
-            nsc_branch = nsc_branch[:j] + bytes([nsc_branch[j] ^ 0x80]) + nsc_branch[j + 1:]
-        if kind == K_BAD_EXEC_BRANCH:
-            j = int(rng.integers(0, 128))
-            a_br = a_br[:j] + bytes([a_br[j] ^ 0x10]) + a_br[j + 1:]
-        cols["att_beacon"][i] = np.frombuffer(a_beacon, np.uint8)
-        cols["att_exec"][i] = np.frombuffer(a_ex, np.uint8)
-        cols["att_branch"][i] = np.frombuffer(a_br, np.uint8)
-        cols["fin_beacon"][i] = np.frombuffer(f_beacon, np.uint8)
-        cols["fin_exec"][i] = np.frombuffer(f_ex, np.uint8)
-        cols["fin_branch"][i] = np.frombuffer(f_br, np.uint8)
-        cols["nsc_branch"][i] = np.frombuffer(nsc_branch, np.uint8)
-        cols["finality_branch"][i] = np.frombuffer(fin_branch, np.uint8)
-        cols["sync_bits"][i] = np.packbits(bits, bitorder="little")
-        sig_slot[i] = ss
         msgs[32 * i:32 * i + 32] = m
         sk_sums[32 * i:32 * i + 32] = (sks or 1).to_bytes(32, "big")
+        bitss.append(np.packbits(bits, bitorder="little").tobytes())
+        pending.append((ss, fin_blk, att_state, att_blk))
     sigs = verifier.sign_batch(np.frombuffer(bytes(sk_sums), np.uint8), np.frombuffer(bytes(msgs), np.uint8))
     for i in np.flatnonzero(kinds == K_BAD_SIG_ENCODING):
         sigs[i, 0] = 0x9a  # compression flag set, x1 >= p
         sigs[i, 1:48] = 0xff
-    cols["sync_signature"][:] = sigs
-    if npool > 1 and with_next:
-        nsc_pool, nsc_index = pool_bytes, (np.arange(n) % npool).astype(np.uint32)
-    else:
-        nsc_pool = np.frombuffer(nxt.ssz if with_next else bytes(L.SYNC_COMMITTEE_BYTES), np.uint8).reshape(1, -1).copy()
-        nsc_index = np.zeros(n, np.uint32)
-    upd = PackedUpdates(nsc_pool=nsc_pool, nsc_index=nsc_index, signature_slot=sig_slot, **cols)
+
+    # pass 2: the signature blocks (carrying the sync aggregates), their states, the derived updates
+    rows = []
+    for i, (ss, fin_blk, att_state, att_blk) in enumerate(pending):
+        kind = int(kinds[i])
+        # (a block without participants cannot be derived from, full-node.md:146: K_NO_PARTICIPANTS rows are
+        # derived with one bit and then cleared, a corruption like the others)
+        bits = b"\x01" + bytes(63) if kind == K_NO_PARTICIPANTS else bitss[i]
+        blk = _block(rng, ss, cfg, parent_root=att_blk.hash_tree_root(), bits=bits, sig=sigs[i].tobytes(),
+                     payload=False)
+        st, blk = _with_state(rng, blk, att_state.finalized_checkpoint_epoch, att_state.finalized_checkpoint_root,
+                              cur.ssz, att_state.next_sync_committee)
+        u = PR.create_light_client_update(st, blk, att_state, att_blk, fin_blk, cfg)
+        if kind == K_NO_PARTICIPANTS:
+            u.sync_committee_bits = bytes(64)
+        if not with_next:
+            u.next_sync_committee = PR.EMPTY_SYNC_COMMITTEE
+            u.next_sync_committee_branch = bytes(L.NSC_BRANCH_BYTES)
+        if kind == K_BAD_FINALITY_BRANCH and with_finality:
+            u.finality_branch = _flip(u.finality_branch, int(rng.integers(0, 192)), 0x01)
+        if kind == K_BAD_NSC_BRANCH and with_next and not sign_next:
+            u.next_sync_committee_branch = _flip(u.next_sync_committee_branch, int(rng.integers(0, 160)), 0x80)
+        if kind == K_BAD_EXEC_BRANCH:
+            h = u.attested_header
+            u.attested_header = PR.HeaderRow(h.beacon, h.execution, _flip(h.execution_branch, int(rng.integers(0, 128)), 0x10))
+        rows.append(u)
+    upd = PR.pack_updates(rows)
     expected = np.array([EXPECTED_REASON[int(k)] for k in kinds], np.uint8)
-    current_slot = int(sig_slot.max()) if n else store_fin + 1
+    current_slot = int(upd.signature_slot.max()) if n else store_fin + 1
     return SyntheticBatch(upd, kinds, expected, store_fin, cur, store_next if npool > 1 else nxt, current_slot, gvr)
+
+
+def _flip(b: bytes, j: int, mask: int) -> bytes:
+    return b[:j] + bytes([b[j] ^ mask]) + b[j + 1:]
 
 
 def tile(sb: SyntheticBatch, reps: int) -> SyntheticBatch:

@@ -177,3 +177,16 @@ def encode_updates(batch: PackedUpdates, kind: str = "update", fork: str = "dene
         fixed = 4 + len(sc) + 4 + len(mid)
         out.append(fixed.to_bytes(4, "little") + sc + (fixed + len(att)).to_bytes(4, "little") + mid + att + fin)
     return out
+
+
+def encode_bootstrap(beacon: bytes, execution: bytes, execution_branch: bytes, committee: bytes,
+                     committee_branch: bytes, fork: str = "deneb") -> bytes:
+    """LightClientBootstrap rows (sync-protocol.md:109-115) -> SSZ wire bytes (inverse of decode_bootstrap)."""
+    if fork not in FORKS:
+        raise ValueError(f"fork must be one of {list(FORKS)}")
+    u8 = lambda b: np.frombuffer(bytes(b), np.uint8)  # noqa: E731
+    if len(committee) != L.SYNC_COMMITTEE_BYTES or len(committee_branch) != 160:
+        raise ValueError("committee must be 24,624 bytes and its branch 5 x 32 bytes")
+    hdr = _encode_header(u8(beacon), u8(execution), u8(execution_branch), fork)
+    fixed = 4 + L.SYNC_COMMITTEE_BYTES + 160
+    return fixed.to_bytes(4, "little") + bytes(committee) + bytes(committee_branch) + hdr

@@ -19,8 +19,8 @@ from types import SimpleNamespace
 from typing import Optional, Sequence
 
 from . import bls12_381 as _bls
-from .ssz import (Bitvector, ByteList, ByteVector, Bytes4, Bytes20, Bytes32, Bytes48, Bytes96, Container,
-                  Vector, hash_tree_root, sha256, uint64, uint256)
+from .ssz import (Bitvector, ByteList, ByteVector, Bytes4, Bytes20, Bytes32, Bytes48, Bytes96, Container, SSZList,
+                  Vector, boolean, compute_merkle_proof, hash_tree_root, sha256, uint8, uint64, uint256)
 
 # ----------------------------------------------------------------------------- mainnet preset/config
 SLOTS_PER_EPOCH = 32
@@ -164,6 +164,136 @@ class CapellaExecutionPayloadHeader(Container):  # capella (15 fields)
 
 
 capella = SimpleNamespace(ExecutionPayloadHeader=CapellaExecutionPayloadHeader)
+
+
+# ----------------------------------------------------------------------------- Deneb beacon chain (producer side)
+# The containers full-node.md's producer functions read (BeaconState, SignedBeaconBlock, ...), restated
+# from upstream deneb/beacon-chain.md with the mainnet preset limits.  Operation lists the fixtures keep
+# empty use an opaque composite element (an empty list's root depends only on its limit).
+class Fork(Container):
+    previous_version: Version
+    current_version: Version
+    epoch: Epoch
+
+
+class Checkpoint(Container):
+    epoch: Epoch
+    root: Root
+
+
+class Eth1Data(Container):
+    deposit_root: Root
+    deposit_count: uint64
+    block_hash: Hash32
+
+
+class Validator(Container):
+    pubkey: BLSPubkey
+    withdrawal_credentials: Bytes32
+    effective_balance: Gwei
+    slashed: boolean
+    activation_eligibility_epoch: Epoch
+    activation_epoch: Epoch
+    exit_epoch: Epoch
+    withdrawable_epoch: Epoch
+
+
+class HistoricalSummary(Container):
+    block_summary_root: Root
+    state_summary_root: Root
+
+
+class Withdrawal(Container):
+    index: uint64
+    validator_index: ValidatorIndex
+    address: ExecutionAddress
+    amount: Gwei
+
+
+class _Opaque(Container):
+    root: Root
+
+
+Transaction = ByteList[2 ** 30]
+
+
+class ExecutionPayload(Container):  # deneb
+    parent_hash: Hash32
+    fee_recipient: ExecutionAddress
+    state_root: Bytes32
+    receipts_root: Bytes32
+    logs_bloom: LogsBloom
+    prev_randao: Bytes32
+    block_number: uint64
+    gas_limit: uint64
+    gas_used: uint64
+    timestamp: uint64
+    extra_data: ExtraData
+    base_fee_per_gas: uint256
+    block_hash: Hash32
+    transactions: SSZList[Transaction, 2 ** 20]
+    withdrawals: SSZList[Withdrawal, 16]
+    blob_gas_used: uint64
+    excess_blob_gas: uint64
+
+
+class BeaconBlockBody(Container):  # deneb (12 fields -> 16 leaves; execution_payload = gindex 25)
+    randao_reveal: BLSSignature
+    eth1_data: Eth1Data
+    graffiti: Bytes32
+    proposer_slashings: SSZList[_Opaque, 16]
+    attester_slashings: SSZList[_Opaque, 2]
+    attestations: SSZList[_Opaque, 128]
+    deposits: SSZList[_Opaque, 16]
+    voluntary_exits: SSZList[_Opaque, 16]
+    sync_aggregate: SyncAggregate
+    execution_payload: ExecutionPayload
+    bls_to_execution_changes: SSZList[_Opaque, 16]
+    blob_kzg_commitments: SSZList[Bytes48, 4096]
+
+
+class BeaconBlock(Container):
+    slot: Slot
+    proposer_index: ValidatorIndex
+    parent_root: Root
+    state_root: Root
+    body: BeaconBlockBody
+
+
+class SignedBeaconBlock(Container):
+    message: BeaconBlock
+    signature: BLSSignature
+
+
+class BeaconState(Container):  # deneb (28 fields -> 32 leaves)
+    genesis_time: uint64
+    genesis_validators_root: Root
+    slot: Slot
+    fork: Fork
+    latest_block_header: BeaconBlockHeader
+    block_roots: Vector[Root, 8192]
+    state_roots: Vector[Root, 8192]
+    historical_roots: SSZList[Root, 2 ** 24]
+    eth1_data: Eth1Data
+    eth1_data_votes: SSZList[Eth1Data, 2048]
+    eth1_deposit_index: uint64
+    validators: SSZList[Validator, 2 ** 40]
+    balances: SSZList[Gwei, 2 ** 40]
+    randao_mixes: Vector[Bytes32, 65536]
+    slashings: Vector[Gwei, 8192]
+    previous_epoch_participation: SSZList[uint8, 2 ** 40]
+    current_epoch_participation: SSZList[uint8, 2 ** 40]
+    justification_bits: Bitvector[4]
+    previous_justified_checkpoint: Checkpoint
+    current_justified_checkpoint: Checkpoint
+    finalized_checkpoint: Checkpoint
+    inactivity_scores: SSZList[uint64, 2 ** 40]
+    current_sync_committee: SyncCommittee
+    next_sync_committee: SyncCommittee
+    latest_execution_payload_header: ExecutionPayloadHeader
+    next_withdrawal_index: uint64
+    next_withdrawal_validator_index: ValidatorIndex
+    historical_summaries: SSZList[HistoricalSummary, 2 ** 24]
 
 
 class ForkData(Container):

@@ -106,10 +106,22 @@ class uint256(uint64):
         return int.__new__(cls, v)
 
 
-class boolean(int):
-    @classmethod
-    def default(cls):
-        return cls(0)
+class uint8(uint64):
+    SIZE = 1
+
+    def __new__(cls, v: int = 0):
+        v = int(v)
+        if not 0 <= v < 2 ** 8:
+            raise ValueError("uint8 out of range")
+        return int.__new__(cls, v)
+
+
+class boolean(uint8):
+    def __new__(cls, v: int = 0):
+        v = int(v)
+        if v not in (0, 1):
+            raise ValueError("boolean is 0 or 1")
+        return int.__new__(cls, v)
 
 
 class _ByteVectorBase(bytes):
@@ -278,6 +290,88 @@ class _VectorFactory:
 
 
 Vector = _VectorFactory()
+
+
+class _ListBase(list):
+    """List[T, N]: basic elements packed, composite elements by root; hash_tree_root mixes in the length."""
+    ELEM: Any = None
+    LIMIT = 0
+
+    def __init__(self, items=()):
+        items = list(items)
+        if len(items) > self.LIMIT:
+            raise ValueError(f"{type(self).__name__} over its limit")
+        super().__init__(self.ELEM(x) if not isinstance(x, self.ELEM) else x for x in items)
+
+    @classmethod
+    def default(cls):
+        return cls()
+
+    @classmethod
+    def is_fixed(cls):
+        return False
+
+    @classmethod
+    def is_basic(cls):
+        return issubclass(cls.ELEM, uint64)
+
+    @classmethod
+    def chunk_limit(cls):
+        return (cls.LIMIT * cls.ELEM.SIZE + 31) // 32 if cls.is_basic() else cls.LIMIT
+
+    @classmethod
+    def data_root(cls, v) -> bytes:
+        if cls.is_basic():
+            return merkleize(pack_bytes(b"".join(cls.ELEM.ser(x) for x in v)), cls.chunk_limit())
+        return merkleize([cls.ELEM.htr(x) for x in v], cls.LIMIT)
+
+    @classmethod
+    def htr(cls, v) -> bytes:
+        return mix_in_length(cls.data_root(v), len(v))
+
+    @classmethod
+    def ser(cls, v) -> bytes:
+        if cls.ELEM.is_fixed():
+            return b"".join(cls.ELEM.ser(x) for x in v)
+        parts = [cls.ELEM.ser(x) for x in v]
+        off = 4 * len(parts)
+        head = bytearray()
+        for p in parts:
+            head += off.to_bytes(4, "little")
+            off += len(p)
+        return bytes(head) + b"".join(parts)
+
+    @classmethod
+    def de(cls, b: bytes):
+        if cls.ELEM.is_fixed():
+            sz = cls.ELEM.fixed_size()
+            if len(b) % sz:
+                raise ValueError("List size")
+            return cls([cls.ELEM.de(b[i:i + sz]) for i in range(0, len(b), sz)])
+        if not b:
+            return cls()
+        first = int.from_bytes(b[:4], "little")
+        if first % 4 or first > len(b):
+            raise ValueError("List offsets")
+        offs = [int.from_bytes(b[i:i + 4], "little") for i in range(0, first, 4)] + [len(b)]
+        if any(offs[k + 1] < offs[k] for k in range(len(offs) - 1)):
+            raise ValueError("List offsets")
+        return cls([cls.ELEM.de(b[offs[k]:offs[k + 1]]) for k in range(len(offs) - 1)])
+
+
+_L_CACHE: Dict[Tuple[Any, int], type] = {}
+
+
+class _ListFactory:
+    def __getitem__(self, params) -> type:
+        elem, n = params
+        key = (elem, n)
+        if key not in _L_CACHE:
+            _L_CACHE[key] = type(f"List[{elem.__name__},{n}]", (_ListBase,), {"ELEM": elem, "LIMIT": n})
+        return _L_CACHE[key]
+
+
+SSZList = _ListFactory()
 
 
 class _BitvectorBase(list):
@@ -474,3 +568,58 @@ def hash_tree_root(value) -> bytes:
 
 def serialize(value) -> bytes:
     return type(value).ser(value)
+
+
+# ----------------------------------------------------------------------------- Merkle proofs
+def _tree_path(chunks: List[bytes], depth: int, idx: int) -> List[bytes]:
+    """Sibling roots on the path to leaf idx of merkleize(chunks) padded to 2^depth, bottom-up."""
+    out = []
+    layer = list(chunks)
+    for d in range(depth):
+        sib = idx ^ 1
+        out.append(layer[sib] if sib < len(layer) else ZERO_HASHES[d])
+        if len(layer) % 2:
+            layer.append(ZERO_HASHES[d])
+        layer = [sha256(layer[i] + layer[i + 1]) for i in range(0, len(layer), 2)]
+        idx >>= 1
+    return out
+
+
+def compute_merkle_proof(obj, gindex: int) -> List[bytes]:
+    """The Merkle branch of the node at generalized index `gindex` inside SSZ object `obj` (bottom-up,
+    the order is_valid_merkle_branch consumes).  Restates the upstream helper the reference declares
+    without a body (full-node.md:35-38) for the containers / vectors / lists of this module."""
+    bits = bin(int(gindex))[3:]
+    node, levels = obj, []
+    while bits:
+        t = type(node)
+        if isinstance(node, _ListBase):          # root = H(data_root, length)
+            if bits[0] == "1":
+                levels.append([t.data_root(node)])
+                assert len(bits) == 1, "nothing below a list's length chunk"
+                bits = ""
+                continue
+            levels.append([len(node).to_bytes(32, "little")])
+            bits = bits[1:]
+            assert not t.is_basic(), "proofs into packed basic lists are not needed here"
+            depth = _next_pow2_depth(t.LIMIT)
+            children, chunks = list(node), [t.ELEM.htr(x) for x in node]
+        elif isinstance(node, Container):
+            depth = _next_pow2_depth(len(t._fields))
+            children = [getattr(node, n) for n, _ in t._fields]
+            chunks = [ft.htr(c) for c, (_, ft) in zip(children, t._fields)]
+        elif isinstance(node, _VectorBase) and not issubclass(t.ELEM, uint64):
+            depth = _next_pow2_depth(t.LENGTH)
+            children, chunks = list(node), [t.ELEM.htr(x) for x in node]
+        else:
+            raise TypeError(f"no Merkle descent into {t.__name__}")
+        take, bits = bits[:depth], bits[depth:]
+        assert len(take) == depth, "generalized index ends inside a subtree"
+        idx = int(take, 2) if take else 0
+        levels.append(_tree_path(chunks, depth, idx))
+        node = children[idx] if idx < len(children) else None
+        assert node is not None or not bits
+    out = []
+    for lv in reversed(levels):
+        out += lv
+    return out

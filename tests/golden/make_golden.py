@@ -42,6 +42,7 @@ from lcv import synth  # noqa: E402
 from lcv.config import MAINNET, TESTNET  # noqa: E402
 from oracle import bls12_381 as B  # noqa: E402
 from oracle import spec as S  # noqa: E402
+from oracle.ssz import serialize  # noqa: E402
 
 REF = "/root/reference/sync-protocol.md"
 COLS = ("att_beacon", "att_exec", "att_branch", "fin_beacon", "fin_exec", "fin_branch", "nsc_branch",
@@ -422,6 +423,194 @@ def make_wire():
     print("wire:", len(msgs), "messages,", len(bmsgs), "bootstraps")
 
 
+# ----------------------------------------------------------------------------- producer side (full-node.md)
+FULL_NODE = "/root/reference/full-node.md"
+
+
+def load_full_node(ns):
+    """exec the reference's full-node.md blocks into `ns` (after sync-protocol.md's), with the oracle's
+    compute_merkle_proof for the helper the reference declares without a body (full-node.md:35-38)."""
+    from oracle.ssz import compute_merkle_proof
+    from typing import Sequence
+    ns.update(BeaconState=S.BeaconState, SignedBeaconBlock=S.SignedBeaconBlock, ALTAIR_FORK_EPOCH=S.ALTAIR_FORK_EPOCH,
+              Sequence=Sequence, SSZObject=object)
+    text = open(FULL_NODE).read()
+    for m in re.finditer(r"```python\n(.*?)```", text, re.S):
+        start_line = text[:m.start(1)].count("\n") + 1
+        exec(compile("\n" * (start_line - 1) + m.group(1), "full-node.md", "exec", dont_inherit=True), ns)
+    ns["compute_merkle_proof"] = compute_merkle_proof
+    return ns
+
+
+def _payload(rng, deneb=True):
+    return S.ExecutionPayload(
+        parent_hash=rng.bytes(32), fee_recipient=rng.bytes(20), state_root=rng.bytes(32), receipts_root=rng.bytes(32),
+        logs_bloom=rng.bytes(256), prev_randao=rng.bytes(32), block_number=int(rng.integers(0, 2 ** 40)),
+        gas_limit=int(rng.integers(0, 2 ** 40)), gas_used=int(rng.integers(0, 2 ** 40)),
+        timestamp=int(rng.integers(0, 2 ** 40)), extra_data=rng.bytes(int(rng.integers(0, 33))),
+        base_fee_per_gas=int(rng.integers(0, 2 ** 62)), block_hash=rng.bytes(32),
+        transactions=[rng.bytes(int(rng.integers(1, 200))) for _ in range(int(rng.integers(0, 4)))],
+        withdrawals=[S.Withdrawal(index=int(rng.integers(0, 2 ** 30)), validator_index=int(rng.integers(0, 2 ** 20)),
+                                  address=rng.bytes(20), amount=int(rng.integers(0, 2 ** 40))) for _ in range(2)],
+        blob_gas_used=int(rng.integers(0, 2 ** 20)) if deneb else 0,
+        excess_blob_gas=int(rng.integers(0, 2 ** 20)) if deneb else 0)
+
+
+def _block_state(rng, slot, parent_root, fin_cp, cur, nxt, bits, sig, gvr):
+    """A (post-state, signed block) pair at `slot` with random contents (Deneb containers)."""
+    body = S.BeaconBlockBody(randao_reveal=rng.bytes(96),
+                             eth1_data=S.Eth1Data(deposit_root=rng.bytes(32), deposit_count=int(rng.integers(0, 2 ** 20)),
+                                                  block_hash=rng.bytes(32)),
+                             graffiti=rng.bytes(32),
+                             sync_aggregate=S.SyncAggregate(sync_committee_bits=list(bits), sync_committee_signature=sig),
+                             execution_payload=_payload(rng), blob_kzg_commitments=[rng.bytes(48) for _ in range(2)])
+    proposer = int(rng.integers(0, 2 ** 20))
+    st = S.BeaconState(
+        genesis_time=1606824023, genesis_validators_root=gvr, slot=slot,
+        fork=S.Fork(previous_version=rng.bytes(4), current_version=rng.bytes(4), epoch=int(rng.integers(0, 2 ** 20))),
+        latest_block_header=S.BeaconBlockHeader(slot=slot, proposer_index=proposer, parent_root=parent_root,
+                                                state_root=bytes(32), body_root=S.hash_tree_root(body)),
+        historical_roots=[rng.bytes(32) for _ in range(3)],
+        eth1_data=S.Eth1Data(deposit_root=rng.bytes(32), deposit_count=7, block_hash=rng.bytes(32)),
+        eth1_deposit_index=int(rng.integers(0, 2 ** 20)),
+        validators=[S.Validator(pubkey=rng.bytes(48), withdrawal_credentials=rng.bytes(32), effective_balance=32 * 10 ** 9,
+                                slashed=k == 1, activation_eligibility_epoch=k, activation_epoch=k + 1,
+                                exit_epoch=2 ** 64 - 1, withdrawable_epoch=2 ** 64 - 1) for k in range(3)],
+        balances=[int(rng.integers(0, 2 ** 40)) for _ in range(3)],
+        previous_epoch_participation=[7, 3, 0], current_epoch_participation=[1, 7, 7],
+        justification_bits=[1, 1, 0, 1],
+        previous_justified_checkpoint=S.Checkpoint(epoch=int(rng.integers(0, 2 ** 20)), root=rng.bytes(32)),
+        current_justified_checkpoint=S.Checkpoint(epoch=int(rng.integers(0, 2 ** 20)), root=rng.bytes(32)),
+        finalized_checkpoint=fin_cp, inactivity_scores=[0, 5, 9],
+        current_sync_committee=H.committee_from(cur), next_sync_committee=H.committee_from(nxt),
+        next_withdrawal_index=int(rng.integers(0, 2 ** 30)), next_withdrawal_validator_index=int(rng.integers(0, 2 ** 20)),
+        historical_summaries=[S.HistoricalSummary(block_summary_root=rng.bytes(32), state_summary_root=rng.bytes(32))])
+    blk = S.BeaconBlock(slot=slot, proposer_index=proposer, parent_root=parent_root, state_root=S.hash_tree_root(st),
+                        body=body)
+    return st, S.SignedBeaconBlock(message=blk, signature=rng.bytes(96))
+
+
+def _state_view_arrays(st):
+    """The sparse producer view of an oracle BeaconState: explicit fields + every field's root."""
+    roots = np.stack([np.frombuffer(bytes(t.htr(getattr(st, n))), np.uint8) for n, t in type(st)._fields])
+    return dict(slot=int(st.slot), header=np.frombuffer(serialize(st.latest_block_header), np.uint8),
+                fin_epoch=int(st.finalized_checkpoint.epoch), fin_root=np.frombuffer(bytes(st.finalized_checkpoint.root), np.uint8),
+                cur=np.frombuffer(serialize(st.current_sync_committee), np.uint8),
+                nxt=np.frombuffer(serialize(st.next_sync_committee), np.uint8), roots=roots)
+
+
+def _block_view_arrays(sb):
+    from types import SimpleNamespace
+    from lcv import layout as LL
+    m = sb.message
+    b = m.body
+    roots = np.stack([np.frombuffer(bytes(t.htr(getattr(b, n))), np.uint8) for n, t in type(b)._fields])
+    pl = b.execution_payload
+    hdr = SimpleNamespace(**{n: getattr(pl, n) for n in LL.EXEC_FIELDS if n not in ("transactions_root", "withdrawals_root")},
+                          transactions_root=S.hash_tree_root(pl.transactions), withdrawals_root=S.hash_tree_root(pl.withdrawals))
+    return dict(slot=int(m.slot), proposer=int(m.proposer_index), parent=np.frombuffer(bytes(m.parent_root), np.uint8),
+                state_root=np.frombuffer(bytes(m.state_root), np.uint8),
+                bits=np.frombuffer(S.SyncAggregate._fields[0][1].ser(b.sync_aggregate.sync_committee_bits), np.uint8),
+                sig=np.frombuffer(bytes(b.sync_aggregate.sync_committee_signature), np.uint8),
+                exec=np.frombuffer(LL.pack_execution(hdr), np.uint8), roots=roots)
+
+
+def make_producer():
+    """producer.npz: light-client data derived by the reference's OWN exec'd full-node.md functions
+    (block_to_light_client_header, create_light_client_bootstrap / _update / _finality_update /
+    _optimistic_update; compute_merkle_proof = the oracle's SSZ proof) from random Deneb-shaped
+    beacon states and blocks (oracle/spec.py containers), with each update's validation reason from the
+    exec'd validate_light_client_update.  Stored: the producer views of every state / block (explicit
+    fields + field roots, what lcv.producer consumes) and the expected SSZ bytes of every output."""
+    from oracle.ssz import serialize
+    v = H.hostsim_verifier()
+    ns, assert_lines = load_reference()
+    load_full_node(ns)
+    cur, nxt = synth.make_committee(v, 0), synth.make_committee(v, 1)
+    gvr = synth.sha256(b"lcv-producer-genesis-validators-root")
+    SPP = MAINNET.SLOTS_PER_PERIOD
+    rng = np.random.default_rng(77)
+    states, blocks, cases = [], [], []
+    outs = {"update": [], "finality": [], "optimistic": [], "bootstrap": []}
+    meta = []
+
+    def add_view(lst, arrays):
+        lst.append(arrays)
+        return len(lst) - 1
+
+    scenarios = [("deneb_full", 1100, "same", "fin", "full"),
+                 ("deneb_next_period_signature", 1100, "next", "fin", "random"),
+                 ("deneb_no_finalized_block", 1101, "same", None, "random"),
+                 ("deneb_genesis_finalized", 1102, "same", "genesis", "full"),
+                 ("bellatrix", 600, "same", "fin", "random")]
+    for name, period, sigp, fin_kind, part in scenarios:
+        base = period * SPP
+        F = base + int(rng.integers(1, 64))
+        A = F + 64 + int(rng.integers(0, 512))
+        Ssl = A + 1 + int(rng.integers(0, 16)) if sigp == "same" else base + SPP + int(rng.integers(0, 32))
+        zero_bits = [True] * 512
+        fin_state, fin_block = _block_state(rng, F, rng.bytes(32), S.Checkpoint(epoch=0, root=bytes(32)), cur.ssz, nxt.ssz,
+                                            zero_bits, rng.bytes(96), gvr)
+        if fin_kind == "fin":
+            fin_cp = S.Checkpoint(epoch=F // 32, root=S.hash_tree_root(fin_block.message))
+            fb = fin_block
+        elif fin_kind == "genesis":
+            fin_block.message.slot = 0
+            fin_cp = S.Checkpoint(epoch=0, root=bytes(32))
+            fb = fin_block
+        else:
+            fin_cp = S.Checkpoint(epoch=F // 32, root=rng.bytes(32))
+            fb = None
+        att_state, att_block = _block_state(rng, A, rng.bytes(32), fin_cp, cur.ssz, nxt.ssz, zero_bits, rng.bytes(96), gvr)
+        # the sync aggregate over the attested header, signed by the committee of the signature period
+        if part == "full":
+            bits = [True] * 512
+        else:
+            bits = [bool(x) for x in rng.integers(0, 2, 512)]
+            bits[0] = True
+        signer = cur if sigp == "same" else nxt
+        sk = sum(k for k, b_ in zip(signer.sks, bits) if b_) % synth.R_ORDER
+        att_hdr = S.BeaconBlockHeader(slot=A, proposer_index=att_block.message.proposer_index,
+                                      parent_root=att_block.message.parent_root, state_root=att_block.message.state_root,
+                                      body_root=S.hash_tree_root(att_block.message.body))
+        msg = synth.signing_root(serialize(att_hdr), Ssl, gvr, MAINNET)
+        sig = v.sign_batch(np.frombuffer(sk.to_bytes(32, "big"), np.uint8), np.frombuffer(msg, np.uint8))[0].tobytes()
+        sig_state, sig_block = _block_state(rng, Ssl, S.hash_tree_root(att_block.message), fin_cp, cur.ssz, nxt.ssz,
+                                            bits, sig, gvr)
+        upd = ns["create_light_client_update"](sig_state, sig_block, att_state, att_block, fb)
+        fu = ns["create_light_client_finality_update"](upd)
+        ou = ns["create_light_client_optimistic_update"](upd)
+        boot = ns["create_light_client_bootstrap"](att_state, att_block)
+        for k, obj in (("update", upd), ("finality", fu), ("optimistic", ou), ("bootstrap", boot)):
+            outs[k].append(serialize(obj))
+        # the update validated by the reference against a store finalized at the start of the period
+        store = ns["LightClientStore"](finalized_header=ns["LightClientHeader"](), current_sync_committee=H.committee_from(cur.ssz),
+                                       next_sync_committee=H.committee_from(nxt.ssz), best_valid_update=None,
+                                       optimistic_header=ns["LightClientHeader"](), previous_max_active_participants=0,
+                                       current_max_active_participants=0)
+        store.finalized_header.beacon.slot = base
+        r = reference_reason(ns, assert_lines, store, upd, Ssl, gvr)
+        ids = [add_view(states, _state_view_arrays(st)) for st in (sig_state, att_state)]
+        bids = [add_view(blocks, _block_view_arrays(b_)) for b_ in (sig_block, att_block, fin_block)]
+        cases.append(dict(name=name, state=ids[0], block=bids[0], attested_state=ids[1], attested_block=bids[1],
+                          finalized_block=bids[2] if fb is not None else -1, store_finalized_slot=base, current_slot=Ssl,
+                          reason=r))
+        print(f"producer {name:30s} update {len(outs['update'][-1])} B, reason {r}", flush=True)
+    arrays = {}
+    for prefix, lst in (("state", states), ("block", blocks)):
+        for k in lst[0]:
+            arrays[f"{prefix}_{k}"] = np.stack([np.asarray(x[k]) for x in lst])
+    for k, lst in outs.items():
+        offs = np.cumsum([0] + [len(m) for m in lst])
+        arrays[f"out_{k}"] = np.frombuffer(b"".join(lst), np.uint8)
+        arrays[f"out_{k}_offsets"] = offs.astype(np.uint64)
+    arrays["current_committee"] = np.frombuffer(cur.ssz, np.uint8)
+    arrays["next_committee"] = np.frombuffer(nxt.ssz, np.uint8)
+    arrays["genesis_validators_root"] = np.frombuffer(gvr, np.uint8)
+    np.savez_compressed(os.path.join(HERE, "producer.npz"), **arrays)
+    json.dump({"cases": cases}, open(os.path.join(HERE, "producer.json"), "w"), indent=1)
+
+
 # ----------------------------------------------------------------------------- non-mainnet configuration
 def _oracle_config(cfg):
     """oracle/spec.use_config keywords for a lcv NetworkConfig."""
@@ -491,6 +680,8 @@ if __name__ == "__main__":
         make_store_sequence()
     elif len(sys.argv) > 1 and sys.argv[1] == "testnet":
         make_testnet_cases()
+    elif len(sys.argv) > 1 and sys.argv[1] == "producer":
+        make_producer()
     elif len(sys.argv) > 1 and sys.argv[1] == "wire":
         make_wire()
     else:
@@ -498,3 +689,4 @@ if __name__ == "__main__":
         make_store_sequence()
         make_wire()
         make_testnet_cases()
+        make_producer()

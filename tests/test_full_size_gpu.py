@@ -42,7 +42,7 @@ def _sample(n, k, seed):
 
 def test_config4_adversarial_million(gpu_verifier):
     from lcv import synth
-    base_n = 65536 if N_FULL >= 65536 else N_FULL
+    base_n = 16384 if N_FULL >= 16384 else N_FULL
     kinds = synth.adversarial_kinds(base_n, seed=5, bad_fraction=0.10)
     sb0 = synth.generate(gpu_verifier, base_n, seed=5, participation="random", kinds=kinds)
     sb = synth.tile(sb0, N_FULL // base_n)
@@ -66,7 +66,7 @@ def test_config4_adversarial_million(gpu_verifier):
 
 def test_config2_random_participation_million(gpu_verifier):
     from lcv import synth
-    base_n = min(32768, N_FULL)
+    base_n = min(8192, N_FULL)
     sb = synth.tile(synth.generate(gpu_verifier, base_n, seed=3, participation="random"), N_FULL // base_n)
     gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     pc = np.unpackbits(sb.updates.sync_bits[:base_n], axis=1).sum(1)
