@@ -136,7 +136,7 @@ LCV_FN void sswu_e2prime(fp2& xo, fp2& yo, const fp2& u) {
 
 
 // map_to_curve = SSWU then the 3-isogeny (used by the signer; verification runs the isogeny and the
-// cofactor clearing as the team program `h2c`, lcv_engine.hpp)
+// cofactor clearing as the SOP program `h2c`, F_sop_h2c)
 LCV_FN void map_to_curve_g2(g2j& r, const fp2& u) {
   fp2 x, y;
   sswu_e2prime(x, y, u);

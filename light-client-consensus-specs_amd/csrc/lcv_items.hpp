@@ -9,10 +9,11 @@
 // Stage map onto the reference's validate_light_client_update (sync-protocol.md:386-465):
 //   item_nsc_team   hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449)
 //   item_pre        every non-BLS assert (:392-449) + signing root (:460-463) -> first failing reason
-//   item_h2c_map + h2c program   hash_to_G2(signing_root)       -+
-//   item_sig + g2sub program     signature decode + subgroup     |  bls.FastAggregateVerify (:464)
-//   item_agg        masked G1 aggregation of participant keys   |
-//   item_miller_team / item_fexp_team (lcv_engine.hpp)  pairing  -+
+//   item_h2c_map + SOP h2c program   hash_to_G2(signing_root)                  -+
+//   item_sig + SOP line walk          signature decode + G2 subgroup check      |  bls.FastAggregate-
+//   item_agg                          masked G1 aggregation of participant keys |  Verify (:464)
+//   SOP lines / miller_acc / fexp     the two-pairing product check             -+
+//   (SOP programs: tools/gen_sop.py -> lcv_sop_programs.inc, interpreter lcv_sop.hpp)
 //   item_verdict    conjunction + reason code
 #pragma once
 #include "lcv_h2c.hpp"
@@ -260,7 +261,7 @@ LCV_FN void ld_g2a(g2a& q, const uint32_t* base, size_t cap, size_t i) {
 
 // hash_to_field + simplified SWU for u_m of update i (item t: i = t >> 1, m = t & 1): the serial part
 // of hash_to_G2 (two Fp exponentiations for the square root), two lanes per update; the isogeny,
-// addition and cofactor clearing run as the team program `h2c` (lcv_engine.hpp)
+// addition, cofactor clearing and affine conversion run as the SOP program `h2c` (F_sop_h2c)
 LCV_FN void item_h2c_map(uint32_t t, const Work& W) {
   const uint32_t i = t >> 1, m = t & 1u;
   h256 msg;
@@ -273,8 +274,8 @@ LCV_FN void item_h2c_map(uint32_t t, const Work& W) {
   soa_st_fp2(W.qmap, W.cap, i, 2 * m + 1, y);
 }
 
-// signature decode (flags, x < p, on-curve square root); the G2 subgroup check runs as the team
-// program `g2sub` (lcv_engine.hpp) and may then downgrade PT_OK to PT_BAD
+// signature decode (flags, x < p, on-curve square root); the G2 subgroup check (psi(Q) == [x]Q) is fused
+// into the signature pairing's SOP line walk (F_sop_lines mode 1), which may downgrade PT_OK to PT_BAD
 LCV_FN void item_sig(uint32_t i, const BatchDev& B, const Work& W) {
   g2a s;
   fp2_zero(s.x);

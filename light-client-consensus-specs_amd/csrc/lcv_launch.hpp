@@ -39,15 +39,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(168))) void k_te
     __syncthreads();
   }
 }
-// Engine functors (F::ENGINE, lcv_functors_eng.hpp) run the prefetching round loop k_eng instead.
-template <class F> __global__ void k_eng(F f, uint32_t n);
-template <class F, class = void> struct lcv_is_engine { static constexpr bool value = false; };
-template <class F> struct lcv_is_engine<F, decltype((void)F::ENGINE)> { static constexpr bool value = F::ENGINE; };
 template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s) {
   constexpr uint32_t G = 64 / F::TEAM;
   const uint32_t blocks = (n + G - 1) / G;
-  if constexpr (lcv_is_engine<F>::value) hipLaunchKernelGGL(k_eng<F>, dim3(blocks), dim3(64), 0, s, f, n);
-  else hipLaunchKernelGGL(k_team<F>, dim3(blocks), dim3(64), 0, s, f, n);
+  hipLaunchKernelGGL(k_team<F>, dim3(blocks), dim3(64), 0, s, f, n);
   return hipGetLastError();
 }
 // SOP functors (lcv_functors_sop.hpp): the k_sop round loop, 64 / TEAM items per one-wave block

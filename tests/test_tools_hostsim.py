@@ -1,6 +1,6 @@
 """CPU checks of the build tooling and of device arithmetic through the host simulation:
-  * tools/gen_programs.py emulates every generated team program (Miller loop, final exponentiation,
-    hash_to_G2 tail, G2 subgroup check) with Python integers against the oracle;
+  * tools/gen_sop.py emulates every SOP program (line walk + fused G2 subgroup check, Miller
+    accumulation, final exponentiation, hash_to_G2 tail) with Python integers against the oracle;
   * tools/opcount.py (the roofline numerator) attributes work to every BLS stage, one mark per kernel;
   * the windowed sqrt exponentiations of lcv_field.hpp vs pow() (host simulation of the device code).
 """
@@ -17,19 +17,23 @@ sys.path.insert(0, os.path.join(H.ROOT, "tools"))
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 
 
-def test_generated_programs_match_oracle():
-    import gen_programs as G
-    progs = [G.make_miller(32), G.make_fexp(16), G.make_h2c(16), G.make_g2sub(16)]
-    G.check_miller(progs[0], 32)
-    G.check_fexp(progs[1])
-    G.check_h2c(progs[2])
-    G.check_g2sub(progs[3])
-    # the committed kernel header is what the generator emits now (no stale program ships)
-    inc = os.path.join(H.PKG, "csrc", "lcv_programs.inc")
-    text = open(inc).read()
+def test_sop_programs_match_oracle():
+    """tools/gen_sop.py emulates every SOP program with Python integers (exact device semantics:
+    Montgomery representatives, unreduced accumulators, REDC, the header's subtraction count) against
+    the oracle's pairing, final exponentiation and hash_to_G2; the committed kernel header is what the
+    generator emits now (no stale program ships)."""
+    import gen_sop as GS
+    progs = GS.build()
     for p in progs:
-        assert f"#define LCV_PROG_{p.name.upper()}_ROUNDS {len(p.rounds)}" in text
-        assert f"#define LCV_PROG_{p.name.upper()}_SLOTS {p.nslots}" in text
+        p.finalize()
+    GS.check_miller(progs[0], progs[1])
+    GS.check_fexp(progs[2])
+    GS.check_h2c(progs[3])
+    text = open(os.path.join(H.PKG, "csrc", "lcv_sop_programs.inc")).read()
+    for p in progs:
+        hdr, _ = p.encode()
+        assert f"#define LCV_SOP_{p.name.upper()}_ROUNDS {len(hdr) // 4}" in text
+        assert f"#define LCV_SOP_{p.name.upper()}_SLOTS {p.nslots}" in text
 
 
 def test_opcount_every_stage():

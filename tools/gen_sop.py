@@ -3,7 +3,7 @@
 Miller loop (line precompute + accumulation) and the final exponentiation of the two-pairing check
 inside FastAggregateVerify (reference call site sync-protocol.md:464).
 
-Why a second engine (round-1's lcv_engine.hpp interprets one Fp multiplication per lane per round):
+Why sums of products (round 1's team interpreter ran one Fp multiplication per lane per round):
 on gfx950 a fully reduced Montgomery product costs 288 v_mad_u64_u32, and an interpreter that issues
 one product per lane per round spends more on operand evaluation, LIN lanes and round latency than on
 the product (profiles/r02_v1: VALU busy 0.42-0.50, 1.0-2.4 waves/SIMD).  Here every lane op is
@@ -446,7 +446,7 @@ def _psi_consts():
 
 def line_program(team=10):
     """One pairing's T walk over |x| (63 doublings, 5 additions; the projective doubling of
-    gen_programs.line_dbl scaled by 4, no halvings), emitting per step the sparse line
+    the projective line doubling scaled by 4, no halvings), emitting per step the sparse line
     (a, b, c) = (c00, c01 * (-xP), c11 * yP), 6 Fp values, io index 6 * step + j."""
     p = Program("lines", team)
     qx, qy = slots2(p, "qx"), slots2(p, "qy")
@@ -616,7 +616,7 @@ def frob_ops(p, a, k, out):
 
 
 def fexp_program(team=12):
-    """f^((p^12 - 1)/r) * 3 exactly as gen_programs.fexp_program (result e^3): easy part
+    """f^((p^12 - 1)/r) * 3 (result e^3): easy part
     (p^6 - 1)(p^2 + 1) with a team-parallel Fp12 inversion, hard part (x-1)^2 (x+p)(x^2+p^2-1) + 3."""
     p = Program("fexp", team)
     f = fp12_slots(p, "f")
@@ -726,10 +726,30 @@ def fexp_program(team=12):
 
 
 # ============================================================================ hash_to_G2 tail
+# 3-isogeny E2' -> E2 of RFC 9380 (App. E.3): coefficients of x_num, x_den, y_num, y_den (lowest degree
+# first, Fp2 pairs (c0, c1); the top coefficient of each denominator is 1)
+ISO_XNUM = [
+    (0x5C759507E8E333EBB5B7A9A47D7ED8532C52D39FD3A042A88B58423C50AE15D5C2638E343D9C71C6238AAAAAAAA97D6,
+     0x5C759507E8E333EBB5B7A9A47D7ED8532C52D39FD3A042A88B58423C50AE15D5C2638E343D9C71C6238AAAAAAAA97D6),
+    (0, 0x11560BF17BAA99BC32126FCED787C88F984F87ADF7AE0C7F9A208C6B4F20A4181472AAA9CB8D555526A9FFFFFFFFC71A),
+    (0x11560BF17BAA99BC32126FCED787C88F984F87ADF7AE0C7F9A208C6B4F20A4181472AAA9CB8D555526A9FFFFFFFFC71E,
+     0x8AB05F8BDD54CDE190937E76BC3E447CC27C3D6FBD7063FCD104635A790520C0A395554E5C6AAAA9354FFFFFFFFE38D),
+    (0x171D6541FA38CCFAED6DEA691F5FB614CB14B4E7F4E810AA22D6108F142B85757098E38D0F671C7188E2AAAAAAAA5ED1, 0),
+]
+ISO_XDEN = [(0, P - 72), (12, P - 12), (1, 0)]
+ISO_YNUM = [
+    (0x1530477C7AB4113B59A4C18B076D11930F7DA5D4A07F649BF54439D87D27E500FC8C25EBF8C92F6812CFC71C71C6D706,
+     0x1530477C7AB4113B59A4C18B076D11930F7DA5D4A07F649BF54439D87D27E500FC8C25EBF8C92F6812CFC71C71C6D706),
+    (0, 0x5C759507E8E333EBB5B7A9A47D7ED8532C52D39FD3A042A88B58423C50AE15D5C2638E343D9C71C6238AAAAAAAA97BE),
+    (0x11560BF17BAA99BC32126FCED787C88F984F87ADF7AE0C7F9A208C6B4F20A4181472AAA9CB8D555526A9FFFFFFFFC71C,
+     0x8AB05F8BDD54CDE190937E76BC3E447CC27C3D6FBD7063FCD104635A790520C0A395554E5C6AAAA9354FFFFFFFFE38F),
+    (0x124C9AD43B6CF79BFBF7043DE3811AD0761B0F37A1E26286B0E977C69AA274524E79097A56DC4BD9E1B371C71C718B10, 0),
+]
+ISO_YDEN = [(P - 432, P - 432), (0, P - 216), (18, P - 18), (1, 0)]
+
+
 def _iso_consts():
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    import gen_programs as GP
-    return GP.ISO_XNUM, GP.ISO_XDEN, GP.ISO_YNUM, GP.ISO_YDEN
+    return ISO_XNUM, ISO_XDEN, ISO_YNUM, ISO_YDEN
 
 
 class G2Ops:
@@ -820,7 +840,7 @@ def g2_slots(p, name=None):
 def h2c_program(team=8):
     """hash_to_G2 after the two SSWU maps (inputs: the affine E2' points m0, m1): 3-isogeny to E2 in
     projective form (xn yd : y yn xd : xd yd), Q0 + Q1, clear_cofactor (RFC 9380 App. G.3:
-    [x^2 - x - 1]P + [x - 1] psi(P) + psi^2(2P), as gen_programs.h2c_program), then affine (hx, hy) and hz."""
+    [x^2 - x - 1]P + [x - 1] psi(P) + psi^2(2P)), then affine (hx, hy) and hz."""
     p = Program("h2c", team)
     XN, XD, YN, YD = _iso_consts()
     m = [(slots2(p, f"m{k}x"), slots2(p, f"m{k}y")) for k in range(2)]

@@ -77,7 +77,7 @@ def main(src, dst, latest=None):
     if latest:
         json.dump(doc, open(latest, "w"), indent=1)
     for k, d in ks.items():
-        if k.startswith("k_eng") or k in ("k_items<F_h2c_map>", "k_items<F_sig>"):
+        if k.startswith("k_sop") or k in ("k_items<F_h2c_map>", "k_items<F_sig>"):
             print(k, {x: d.get(x) for x in ("hbm_bytes_per_launch", "valu_busy", "issue_busy",
                                               "mean_waves_per_simd", "lds_bank_conflict_rate", "valu_insts_per_wave")})
 

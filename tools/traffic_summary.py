@@ -33,7 +33,7 @@ def main(src: str, dst: str) -> None:
             e[f"{counter}_KB_per_launch"] = round(s / n, 1)
             e["launches"] = n
     json.dump(out, open(dst, "w"), indent=1)
-    print(json.dumps({k: v for k, v in out.items() if k.startswith("k_eng")}, indent=1))
+    print(json.dumps({k: v for k, v in out.items() if k.startswith("k_sop")}, indent=1))
 
 
 if __name__ == "__main__":
