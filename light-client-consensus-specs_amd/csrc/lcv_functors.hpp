@@ -19,7 +19,14 @@ struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32
 struct F_agg_fold { Work W; uint32_t m; LCV_HD void operator()(uint32_t) const { item_agg_fold(m, W); } };
 struct F_verdict { Work W; LCV_HD void operator()(uint32_t i) const { item_verdict(i, W); } };
 struct F_key { CommitteeDev C; LCV_HD void operator()(uint32_t t) const { item_committee_key(t, C); } };
-struct F_sum { CommitteeDev C; LCV_HD void operator()(uint32_t c) const { item_committee_sum(c, C); } };
+struct F_sum {  // one wave per committee (item_committee_sum_team)
+  CommitteeDev C;
+  static constexpr uint32_t TEAM = SUM_TEAM, LDS_WORDS = SUM_LDS, SHARED_WORDS = 0;
+  LCV_HD uint32_t rounds() const { return SUM_ROUNDS; }
+  LCV_HD void operator()(uint32_t c, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t*) const {
+    item_committee_sum_team(c, lane, r, lds, C);
+  }
+};
 
 struct F_msg_import {  // 32-byte messages -> W.msg (big-endian words, SoA)
   const uint8_t* msg; Work W;

@@ -376,15 +376,27 @@ LCV_FN void item_committee_key(uint32_t t, const CommitteeDev& C) {
   C.key_status[t] = (uint8_t)st;
 }
 
-// per committee: sum of all valid keys (for the complement trick) and the invalid-key bitmap
-LCV_FN void item_committee_sum(uint32_t c, const CommitteeDev& C) {
-  g1j acc;
-  jac_set_inf(acc);
-  const uint32_t* pts = C.pts + (size_t)c * 512 * 24;
-  LCV_NOUNROLL for (int w = 0; w < 16; ++w) {
+// per committee: sum of all valid keys (for the complement trick) and the invalid-key bitmap, on a
+// team of 64 lanes (one wave per committee): round 0, lane l sums keys 8l .. 8l + 7 and records their
+// validity byte; rounds 1..6, a pairwise tree over the 64 partial sums in LDS (lane l adds lane
+// l + 2^(k-1)'s sum when l % 2^k == 0); round 7 writes the sum and the 16 mask words.
+enum { SUM_TEAM = 64, SUM_ROUNDS = 8, SUM_LDS = 64 * 36 + 16 };
+LCV_FN void ld_g1j_lds(g1j& p, const uint32_t* s) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { p.x.v[k] = s[k]; p.y.v[k] = s[12 + k]; p.z.v[k] = s[24 + k]; }
+}
+LCV_FN void st_g1j_lds(uint32_t* s, const g1j& p) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { s[k] = p.x.v[k]; s[12 + k] = p.y.v[k]; s[24 + k] = p.z.v[k]; }
+}
+LCV_FN void item_committee_sum_team(uint32_t c, uint32_t lane, uint32_t r, uint32_t* lds, const CommitteeDev& C) {
+  uint32_t* part = lds + 36 * lane;
+  uint8_t* mbytes = (uint8_t*)(lds + 64 * 36);
+  if (r == 0) {
+    g1j acc;
+    jac_set_inf(acc);
+    const uint32_t* pts = C.pts + (size_t)c * 512 * 24;
     uint32_t m = 0;
-    LCV_NOUNROLL for (int b = 0; b < 32; ++b) {
-      const int j = 32 * w + b;
+    LCV_NOUNROLL for (int b = 0; b < 8; ++b) {
+      const uint32_t j = 8 * lane + b;
       if (C.key_status[(size_t)c * 512 + j] != PT_OK) {
         m |= 1u << b;
         continue;
@@ -393,10 +405,27 @@ LCV_FN void item_committee_sum(uint32_t c, const CommitteeDev& C) {
       ld_g1a_tbl(p, pts, j);
       jac_madd(acc, acc, p);
     }
-    C.badmask[c * 16 + w] = m;
+    st_g1j_lds(part, acc);
+    mbytes[lane] = (uint8_t)m;
+  } else if (r < 7) {
+    const uint32_t step = 1u << (r - 1);
+    if ((lane & (2 * step - 1)) == 0) {
+      g1j a, b;
+      ld_g1j_lds(a, part);
+      ld_g1j_lds(b, lds + 36 * (lane + step));
+      jac_add(a, a, b);
+      st_g1j_lds(part, a);
+    }
+  } else {
+    if (lane < 16) {
+      const uint32_t* mw = (const uint32_t*)mbytes;  // bytes 4w .. 4w + 3 = keys 32w .. 32w + 31
+      C.badmask[c * 16 + lane] = mw[lane];
+    }
+    if (lane == 0) {
+      uint32_t* s = C.sum_all + 36 * c;
+      LCV_UNROLL for (int k = 0; k < 36; ++k) s[k] = lds[k];
+    }
   }
-  uint32_t* s = C.sum_all + 36 * c;
-  LCV_UNROLL for (int k = 0; k < 12; ++k) { s[k] = acc.x.v[k]; s[12 + k] = acc.y.v[k]; s[24 + k] = acc.z.v[k]; }
 }
 
 }  // namespace lcv

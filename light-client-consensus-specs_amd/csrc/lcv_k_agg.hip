@@ -6,4 +6,4 @@
 
 LCV_INSTANTIATE(F_agg)
 LCV_INSTANTIATE(F_agg_fold)
-LCV_INSTANTIATE(F_sum)
+LCV_INSTANTIATE_TEAM(F_sum)

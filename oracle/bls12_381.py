@@ -380,6 +380,18 @@ def g2_psi(p: G2Point) -> G2Point:
     return (f2_mul(f2_conj(p[0]), PSI_CX), f2_mul(f2_conj(p[1]), PSI_CY))
 
 
+G1_BETA = 0x5F19672FDF76CE51BA69C6076A0F77EADDB3A93BE6F89688DE17D813620A00022E01FFFFFFFEFFFE
+H1 = 0x396C8C005555E1568C00AAAB0000AAAB  # #E1(Fp) / r = 3 * 11^2 * 10177^2 * 859267^2 * 52437899^2
+
+
+def g1_in_subgroup_phi(p: G1Point) -> bool:
+    """Scott's test phi(P) == [-x^2]P with phi(x, y) = (beta x, y) (the GPU's KeyValidate test);
+    cross-checked against r*P in tests."""
+    if p is None or not g1_on_curve(p):
+        return False
+    return (G1_BETA * p[0] % P, p[1]) == g1_neg(g1_mul(p, X * X))
+
+
 def g2_in_subgroup_psi(p: G2Point) -> bool:
     """Scott's test psi(P) == [x]P (the GPU's test); cross-checked against r*P in tests."""
     return g2_on_curve(p) and g2_psi(p) == g2_mul(p, X)

@@ -179,7 +179,29 @@ def _bad_keys():
         "off_curve": bytes([0x80 | (x >> 376)]) + _be48(x)[1:],
         "non_subgroup": B.g1_compress(ns),
         "all_zero": bytes(48),
+        # points whose order is a cofactor prime (3, 11, 10177) and a G1 point plus an order-11 point:
+        # each exercises the device's phi(P) == [-x^2]P membership test against r*P == O
+        "order3": B.g1_compress(_cofactor_point(3)),
+        "order11": B.g1_compress(_cofactor_point(11)),
+        "order10177": B.g1_compress(_cofactor_point(10177)),
+        "g1_plus_order11": B.g1_compress(B.g1_add(B.g1_mul(B.G1_GEN, 12345), _cofactor_point(11))),
     }
+
+
+def _cofactor_point(ell: int):
+    """A point of E1(Fp) of order ell (a prime factor of the cofactor h1; ell^2 divides h1 for ell > 3,
+    and E1(Fp)'s ell-part is then Z/ell x Z/ell, of exponent ell)."""
+    k = B.H1 * B.R // (ell if ell == 3 else ell * ell)
+    x = 1
+    while True:
+        x += 1
+        y = B.fp_sqrt((x * x * x + B.B1) % P)
+        if y is None:
+            continue
+        t = B.g1_mul((x, y), k)
+        if t is not None:
+            assert B.g1_mul(t, ell) is None
+            return t
 
 
 def test_g1_key_validate_edges(gpu_verifier):

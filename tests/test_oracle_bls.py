@@ -72,6 +72,40 @@ def test_curve_identities():
     assert not B.g2_in_subgroup((X, y)) and not B.g2_in_subgroup_psi((X, y))
 
 
+def test_g1_membership_phi_matches_definition():
+    """KeyValidate's G1 membership test on the device is phi(P) == [-x^2]P: it agrees with r*P == O on
+    members, on points whose order has each prime factor of the cofactor h1, and on mixed points."""
+    import random
+    rng = random.Random(7)
+    assert B.H1 == 3 * 11 ** 2 * 10177 ** 2 * 859267 ** 2 * 52437899 ** 2
+    assert pow(B.G1_BETA, 3, B.P) == 1
+
+    def curve_point():
+        while True:
+            x = rng.randrange(B.P)
+            y = B.fp_sqrt((x ** 3 + B.B1) % B.P)
+            if y is not None:
+                return (x, y)
+    seen = set()
+    for _ in range(3):
+        g = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+        assert B.g1_in_subgroup(g) and B.g1_in_subgroup_phi(g)
+        q = curve_point()
+        for ell in (3, 11, 10177, 859267, 52437899, B.H1):
+            # E1(Fp)'s ell-part is Z/ell x Z/ell for the squared primes: [h1 r / ell^2]Q has order ell
+            t = B.g1_mul(q, B.H1 * B.R // (ell if ell in (3, B.H1) else ell * ell))
+            if t is None:
+                continue
+            if ell != B.H1:
+                assert B.g1_mul(t, ell) is None
+            seen.add(ell)
+            assert not B.g1_in_subgroup(t) and not B.g1_in_subgroup_phi(t), ell
+            m = B.g1_add(g, t)
+            assert not B.g1_in_subgroup(m) and not B.g1_in_subgroup_phi(m), ell
+        assert B.g1_in_subgroup(q) == B.g1_in_subgroup_phi(q)
+    assert seen >= {3, 11, 10177, 859267, 52437899}
+
+
 def test_bilinearity():
     a, b = 0x1D5E7, 0x2B9F3
     e = B.pairing(B.G1_GEN, B.G2_GEN)
