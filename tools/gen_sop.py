@@ -764,19 +764,26 @@ class G2Ops:
         self.one = T(p.const(1))
 
     def dbl(self, P, out):
-        """out = 2P: t0 = Y^2, t1 = YZ, t2 = b3 Z^2, XY; X3 = 2 (t0 - 3 t2) XY, Y3 = t0^2 + 6 t0 t2 - 3 t2^2,
-        Z3 = 8 t0 t1.  Two rounds (8 + 6 lanes); `out` may be P (in place)."""
+        """out = 2P (RCB Alg. 9, a = 0) scaled by 3, which leaves the projective point unchanged:
+        with t0 = Y^2, t1 = YZ, w = 3 b3 Z^2 = 36 xi Z^2 and XY,
+            X3 = 6 XY (t0 - w),  Y3 = 3 (t0 + w)^2 - 4 w^2,  Z3 = 24 t0 t1
+        (RCB's X3 = 2 XY (t0 - 3 t2), Y3 = t0^2 + 6 t0 t2 - 3 t2^2, Z3 = 8 t0 t1 with t2 = b3 Z^2, times 3).
+        Two rounds (8 ops of <= 2 products, then 6 ops of <= 3); `out` may be P (in place)."""
         p = self.p
         X, Y, Z = P
-        t0, t1, t2, xy = self.t[:4]
+        t0, t1, w, xy = self.t[:4]
         p.round([Op(dst_of(t0[c]), fp2_sqr(Y, c)) for c in range(2)] +
                 [Op(dst_of(t1[c]), fp2_prod(Y, Z, c)) for c in range(2)] +
-                [Op(dst_of(t2[c]), fp2_sqr(Z, c, xi=True, m=12)) for c in range(2)] +
+                [Op(dst_of(w[c]), fp2_sqr(Z, c, xi=True, m=36)) for c in range(2)] +
                 [Op(dst_of(xy[c]), fp2_prod(X, Y, c)) for c in range(2)])
-        ops = [Op(dst_of(out[0][c]), fp2_prod(t0, xy, c, m=2) + fp2_prod(t2, xy, c, m=-6)) for c in range(2)]
-        ops += [Op(dst_of(out[1][c]), fp2_sqr(t0, c) + fp2_prod(t0, t2, c, m=6) + fp2_sqr(t2, c, m=-3))
-                for c in range(2)]
-        ops += [Op(dst_of(out[2][c]), fp2_prod(t0, t1, c, m=8)) for c in range(2)]
+        (a0, a1), (w0, w1), (x0, x1) = t0, w, xy
+        d0, d1 = [a0, ~w0], [a1, ~w1]            # t0 - w
+        s0, s1 = [a0, w0], [a1, w1]              # t0 + w
+        ops = [Op(dst_of(out[0][0]), [(d0, [x0], 6), (d1, [x1], -6)]),
+               Op(dst_of(out[0][1]), [(d0, [x1], 6), (d1, [x0], 6)]),
+               Op(dst_of(out[1][0]), [(s0, s0, 3), (s1, s1, -3), ([w0, w1], [w0, ~w1], -4)]),
+               Op(dst_of(out[1][1]), [(s0, s1, 6), ([w0], [w1], -8)])]
+        ops += [Op(dst_of(out[2][c]), fp2_prod(t0, t1, c, m=24)) for c in range(2)]
         p.round(ops)
 
     def add(self, P1, P2, out):
