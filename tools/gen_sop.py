@@ -125,18 +125,31 @@ class Program:
 
     def round(self, ops):
         """Append one round; more ops than lanes are split into consecutive rounds, which is only
-        exact when no op of a later part reads a slot an earlier part writes (checked)."""
+        exact when no op of a later part reads a slot an earlier part writes (checked).  A split
+        round is cut after sorting its ops by product count (a round costs its largest K on every
+        lane), unless that order would read a slot an earlier part wrote; then the given order."""
         ops = [o for o in ops if o is not None]
         assert ops
         dsts = [o.dst for o in ops] + [o.load[0] for o in ops if o.load]
         assert len(dsts) == len(set(dsts)), "two ops of a round write one slot"
-        written = set()
-        for k in range(0, len(ops), self.team):
-            part = ops[k:k + self.team]
-            reads = {t.slot for o in part for x, y, _ in o.prods for t in x + y} | {s_ for o in part for s_, _ in o.adds}
-            assert not (reads & written), f"{self.name}: split round reads a slot an earlier part wrote"
-            written |= {o.dst for o in part}
-            self.rounds.append(part)
+
+        def parts(order):
+            out, written = [], set()
+            for k in range(0, len(order), self.team):
+                part = order[k:k + self.team]
+                reads = {t.slot for o in part for x, y, _ in o.prods for t in x + y} | {s_ for o in part for s_, _ in o.adds}
+                if reads & written:
+                    return None
+                written |= {o.dst for o in part}
+                out.append(part)
+            return out
+        split = None
+        if len(ops) > self.team:
+            split = parts(sorted(ops, key=lambda o: -len(o.prods)))
+        if split is None:
+            split = parts(ops)
+        assert split is not None, f"{self.name}: split round reads a slot an earlier part wrote"
+        self.rounds.extend(split)
 
     # ------------------------------------------------------------ finalise: slot numbers of constants
     def finalize(self):
