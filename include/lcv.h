@@ -170,13 +170,19 @@ int lcv_bootstrap_check_batch(lcv_ctx* ctx, const uint8_t* beacon112, const uint
  * :120-133 LightClientUpdate, :138-148 LightClientFinalityUpdate, :153-160 LightClientOptimisticUpdate)
  * as received over Req/Resp / gossip (p2p-interface.md).  kind: 0 update, 1 finality update,
  * 2 optimistic update (converted as sync-protocol.md:563-571 / :582-590 do); fork: 0 Deneb
- * ExecutionPayloadHeader (17 fields), 1 Capella (15).  Message i = buf[offsets[i] .. + lengths[i]] ->
+ * ExecutionPayloadHeader (17 fields), 1 Capella (15), 2 Altair (LightClientHeader = beacon only; the
+ * row is its Capella upgrade: empty execution and branch).  Message i = buf[offsets[i] .. + lengths[i]] ->
  * row i of `out` (caller-allocated columns of n rows; out->nsc_pool is ignored).  status[i] = 0 ok,
  * 1 malformed (row zeroed).  Distinct next_sync_committee values: pool row k is the committee at
  * buf + pool_src[k] (UINT64_MAX = SyncCommittee()), *npool_out rows (<= n + 1). */
 int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
                            int kind, int fork, const lcv_update_batch* out, uint64_t* pool_src,
                            uint64_t* npool_out, uint8_t* status);
+/* the same with a fork per message (a Req/Resp response's chunks each carry their own ForkDigest
+ * context, p2p-interface.md:189-200, so one response may straddle a fork boundary) */
+int lcv_ssz_decode_updates_mixed(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+                                 int kind, const uint8_t* forks, const lcv_update_batch* out, uint64_t* pool_src,
+                                 uint64_t* npool_out, uint8_t* status);
 int lcv_ssz_decode_bootstrap(const uint8_t* buf, uint64_t len, int fork, uint8_t* beacon112, uint8_t* exec832,
                              uint8_t* exec_branch128, uint8_t* committee24624, uint8_t* committee_branch160,
                              uint8_t* status);

@@ -91,11 +91,49 @@ void zero_row(const Row& r) {
   const_cast<uint64_t*>(b->signature_slot)[r.i] = 0;
 }
 
+enum { FORK_DENEB = 0, FORK_CAPELLA = 1, FORK_ALTAIR = 2 };
+
+// Altair-format messages (ALTAIR .. BELLATRIX fork versions, p2p-interface.md:82-85, 112-115, 157-160,
+// 197-200): LightClientHeader = {beacon} is fixed-size, so every container is fixed-size.  The rows
+// are the Capella upgrade of the data (upgrade_lc_header_to_capella: empty execution and branch).
+bool decode_one_altair(const uint8_t* p, uint64_t len, int kind, const Row& r, uint64_t* committee) {
+  const lcv_update_batch* b = r.b;
+  const uint64_t size = kind == 0 ? kBeacon + kCommittee + kNscBranch + kBeacon + kFinBranch + kBits + kSig + 8
+                        : kind == 1 ? kBeacon + kBeacon + kFinBranch + kBits + kSig + 8
+                                    : kBeacon + kBits + kSig + 8;
+  if (len != size) return false;
+  uint64_t pos = 0;
+  std::memcpy(r.at(b->attested.beacon, kBeacon), p, kBeacon);
+  pos += kBeacon;
+  if (kind == 0) {
+    *committee = pos;
+    pos += kCommittee;
+    std::memcpy(r.at(b->nsc_branch, kNscBranch), p + pos, kNscBranch);
+    pos += kNscBranch;
+  }
+  if (kind != 2) {
+    std::memcpy(r.at(b->finalized.beacon, kBeacon), p + pos, kBeacon);
+    pos += kBeacon;
+    std::memcpy(r.at(b->finality_branch, kFinBranch), p + pos, kFinBranch);
+    pos += kFinBranch;
+  }
+  std::memcpy(r.at(b->sync_bits, kBits), p + pos, kBits);
+  pos += kBits;
+  std::memcpy(r.at(b->sync_signature, kSig), p + pos, kSig);
+  pos += kSig;
+  uint64_t slot;
+  std::memcpy(&slot, p + pos, 8);
+  const_cast<uint64_t*>(b->signature_slot)[r.i] = slot;
+  return true;
+}
+
 // Decodes one message into row r; *committee = offset (within the message) of next_sync_committee,
 // or UINT64_MAX when the message carries none.
-bool decode_one(const uint8_t* p, uint64_t len, int kind, bool deneb, const Row& r, uint64_t* committee) {
+bool decode_one(const uint8_t* p, uint64_t len, int kind, int fork, const Row& r, uint64_t* committee) {
   const lcv_update_batch* b = r.b;
   *committee = UINT64_MAX;
+  if (fork == FORK_ALTAIR) return decode_one_altair(p, len, kind, r, committee);
+  const bool deneb = fork == FORK_DENEB;
   uint64_t fixed, att_off_pos, fin_off_pos = 0, pos;
   if (kind == 0) fixed = 4 + kCommittee + kNscBranch + 4 + kFinBranch + kBits + kSig + 8;  // 25152
   else if (kind == 1) fixed = 4 + 4 + kFinBranch + kBits + kSig + 8;                       // 368
@@ -182,17 +220,18 @@ template <class Fn> void parallel_rows(uint64_t n, Fn fn) {
 
 }  // namespace
 
-extern "C" int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths,
-                                      uint64_t n, int kind, int fork, const lcv_update_batch* out,
-                                      uint64_t* pool_src, uint64_t* npool_out, uint8_t* status) {
+// the batch decode; fork_of(i) gives message i's fork (one per call, or one per Req/Resp chunk)
+template <class ForkOf>
+static int decode_updates(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths, uint64_t n, int kind,
+                          ForkOf fork_of, const lcv_update_batch* out, uint64_t* pool_src, uint64_t* npool_out,
+                          uint8_t* status) {
   if ((n && (!buf || !offsets || !lengths || !out || !pool_src || !status)) || !npool_out) return LCV_EINVAL;
-  if (kind < 0 || kind > 2 || fork < 0 || fork > 1) return LCV_EINVAL;
+  if (kind < 0 || kind > 2) return LCV_EINVAL;
   if (n && (!out->attested.beacon || !out->attested.execution || !out->attested.exec_branch ||
             !out->finalized.beacon || !out->finalized.execution || !out->finalized.exec_branch ||
             !out->nsc_index || !out->nsc_branch || !out->finality_branch || !out->sync_bits ||
             !out->sync_signature || !out->signature_slot))
     return LCV_EINVAL;
-  const bool deneb = fork == 0;
   constexpr uint64_t kNone = UINT64_MAX;
   std::vector<uint64_t> csrc(n, kNone), key(n, 0);  // committee offset in buf (kNone: SyncCommittee())
   // 1. decode every row (parallel)
@@ -201,7 +240,9 @@ extern "C" int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offset
       const Row r{out, i};
       zero_row(r);
       uint64_t c = kNone;
-      const bool ok = decode_one(buf + offsets[i], lengths[i], kind, deneb, r, &c);
+      const int fork = fork_of(i);
+      const bool ok = fork >= FORK_DENEB && fork <= FORK_ALTAIR &&
+                      decode_one(buf + offsets[i], lengths[i], kind, fork, r, &c);
       status[i] = ok ? 0 : 1;
       if (!ok) {
         zero_row(r);
@@ -249,6 +290,22 @@ extern "C" int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offset
   return LCV_OK;
 }
 
+extern "C" int lcv_ssz_decode_updates(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths,
+                                      uint64_t n, int kind, int fork, const lcv_update_batch* out,
+                                      uint64_t* pool_src, uint64_t* npool_out, uint8_t* status) {
+  if (fork < FORK_DENEB || fork > FORK_ALTAIR) return LCV_EINVAL;
+  return decode_updates(buf, offsets, lengths, n, kind, [fork](uint64_t) { return fork; }, out, pool_src, npool_out,
+                        status);
+}
+
+extern "C" int lcv_ssz_decode_updates_mixed(const uint8_t* buf, const uint64_t* offsets, const uint64_t* lengths,
+                                            uint64_t n, int kind, const uint8_t* forks, const lcv_update_batch* out,
+                                            uint64_t* pool_src, uint64_t* npool_out, uint8_t* status) {
+  if (n && !forks) return LCV_EINVAL;
+  return decode_updates(buf, offsets, lengths, n, kind, [forks](uint64_t i) { return (int)forks[i]; }, out, pool_src,
+                        npool_out, status);
+}
+
 // LightClientBootstrap (sync-protocol.md:109-115): header (offset) | current_sync_committee (24624) |
 // current_sync_committee_branch (5 x 32) | header.  Input of initialize_light_client_store (:351-373).
 extern "C" int lcv_ssz_decode_bootstrap(const uint8_t* buf, uint64_t len, int fork, uint8_t* beacon112,
@@ -256,13 +313,25 @@ extern "C" int lcv_ssz_decode_bootstrap(const uint8_t* buf, uint64_t len, int fo
                                         uint8_t* committee_branch160, uint8_t* status) {
   if (!buf || !beacon112 || !exec832 || !exec_branch128 || !committee24624 || !committee_branch160 || !status)
     return LCV_EINVAL;
-  if (fork < 0 || fork > 1) return LCV_EINVAL;
+  if (fork < FORK_DENEB || fork > FORK_ALTAIR) return LCV_EINVAL;
   constexpr uint64_t fixed = 4 + kCommittee + kNscBranch;  // 24788
-  bool ok = len >= fixed && rd32(buf) == fixed &&
-            decode_header(buf + fixed, len - fixed, fork == 0, beacon112, exec832, exec_branch128);
+  bool ok;
+  uint64_t cpos = 4;
+  if (fork == FORK_ALTAIR) {  // header (112, fixed) | committee | branch
+    ok = len == kBeacon + kCommittee + kNscBranch;
+    if (ok) {
+      std::memcpy(beacon112, buf, kBeacon);
+      std::memset(exec832, 0, kExecRec);
+      std::memset(exec_branch128, 0, kExecBranch);
+    }
+    cpos = kBeacon;
+  } else {
+    ok = len >= fixed && rd32(buf) == fixed &&
+         decode_header(buf + fixed, len - fixed, fork == FORK_DENEB, beacon112, exec832, exec_branch128);
+  }
   if (ok) {
-    std::memcpy(committee24624, buf + 4, kCommittee);
-    std::memcpy(committee_branch160, buf + 4 + kCommittee, kNscBranch);
+    std::memcpy(committee24624, buf + cpos, kCommittee);
+    std::memcpy(committee_branch160, buf + cpos + kCommittee, kNscBranch);
   } else {
     std::memset(beacon112, 0, kBeacon);
     std::memset(exec832, 0, kExecRec);

@@ -77,6 +77,8 @@ SIGNATURES = {
     "lcv_bootstrap_check_batch": (C.c_int, [C.c_void_p, u8p, u8p, u8p, u8p, u8p, u8p, C.c_uint64, u8p]),
     "lcv_ssz_decode_updates": (C.c_int, [u8p, u64p, u64p, C.c_uint64, C.c_int, C.c_int, C.POINTER(UpdateBatch),
                                          u64p, u64p, u8p]),
+    "lcv_ssz_decode_updates_mixed": (C.c_int, [u8p, u64p, u64p, C.c_uint64, C.c_int, u8p, C.POINTER(UpdateBatch),
+                                               u64p, u64p, u8p]),
     "lcv_ssz_decode_bootstrap": (C.c_int, [u8p, C.c_uint64, C.c_int, u8p, u8p, u8p, u8p, u8p, u8p]),
     "lcv_sk_to_pk_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p]),
     "lcv_sign_batch": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint64, u8p]),

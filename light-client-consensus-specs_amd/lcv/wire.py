@@ -9,6 +9,9 @@ csrc/lcv_wire.cpp: host C++, strict SSZ offset rules) directly into the `PackedU
 device verifier consumes; no per-update Python objects are built.
 
     decode_updates(messages, kind="update", fork="deneb")  -> PackedUpdates   (ValueError if malformed)
+        fork: "deneb" | "capella" | "altair" for every message, or one per message (a Req/Resp
+        response's chunks each carry a ForkDigest context: p2p-interface.md:189-200; `fork_of_digest_version`
+        maps a chunk's fork version to its name under the network configuration)
     decode_updates_status(messages, kind, fork)             -> (PackedUpdates, ok: np.ndarray[bool])
     decode_bootstrap(data, fork="deneb")                    -> Bootstrap (header rows, committee, branch)
     encode_updates(batch, kind="update", fork="deneb")      -> [bytes]  (serving side; inverse of decode)
@@ -31,7 +34,35 @@ from ._native import HeaderCols, Lib, UpdateBatch, load, ptr
 from .device import PackedUpdates
 
 KINDS = {"update": 0, "finality": 1, "optimistic": 2}
-FORKS = {"deneb": 0, "capella": 1}
+FORKS = {"deneb": 0, "capella": 1, "altair": 2}  # altair: LightClientHeader = {beacon}; rows = its Capella upgrade
+
+
+def fork_of_digest_version(version: bytes, cfg=None) -> str:
+    """The light-client container namespace of a message whose ForkDigest context is `version`
+    (p2p-interface.md:82-85 / 112-115 / 157-160 / 197-200): ALTAIR..BELLATRIX -> "altair",
+    CAPELLA -> "capella", DENEB and later -> "deneb"."""
+    from . import config as _config
+    cfg = cfg or _config.active()
+    v = bytes(version)
+    if v in (cfg.ALTAIR_FORK_VERSION, cfg.BELLATRIX_FORK_VERSION):
+        return "altair"
+    if v == cfg.CAPELLA_FORK_VERSION:
+        return "capella"
+    if v == cfg.DENEB_FORK_VERSION:
+        return "deneb"
+    raise ValueError(f"no light-client data for fork version {v.hex()}")
+
+
+def _fork_codes(fork, n: int):
+    """One fork code for the call, or a per-message uint8 array."""
+    if isinstance(fork, str):
+        if fork not in FORKS:
+            raise ValueError(f"fork must be one of {list(FORKS)}")
+        return FORKS[fork], None
+    forks = list(fork)
+    if len(forks) != n or any(f not in FORKS for f in forks):
+        raise ValueError(f"fork must be a name or one of {list(FORKS)} per message")
+    return None, np.array([FORKS[f] for f in forks], np.uint8)
 
 Messages = Union[Sequence[bytes], Tuple[np.ndarray, np.ndarray, np.ndarray]]
 
@@ -58,13 +89,14 @@ def _flatten(messages: Messages) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     return buf, offs, lens
 
 
-def decode_updates_status(messages: Messages, kind: str = "update", fork: str = "deneb",
+def decode_updates_status(messages: Messages, kind: str = "update", fork="deneb",
                           lib: Optional[Lib] = None) -> Tuple[PackedUpdates, np.ndarray]:
     """Decode n SSZ messages -> (PackedUpdates, ok); malformed messages give all-zero rows, ok False."""
-    if kind not in KINDS or fork not in FORKS:
-        raise ValueError(f"kind must be one of {list(KINDS)}, fork one of {list(FORKS)}")
+    if kind not in KINDS:
+        raise ValueError(f"kind must be one of {list(KINDS)}")
     buf, offs, lens = _flatten(messages)
     n = int(offs.size)
+    fcode, forks = _fork_codes(fork, n)
     cols = {k: np.zeros((n, w), np.uint8) for k, w in (
         ("att_beacon", L.BEACON_BYTES), ("att_exec", L.EXEC_BYTES), ("att_branch", L.EXEC_BRANCH_BYTES),
         ("fin_beacon", L.BEACON_BYTES), ("fin_exec", L.EXEC_BYTES), ("fin_branch", L.EXEC_BRANCH_BYTES),
@@ -87,9 +119,15 @@ def decode_updates_status(messages: Messages, kind: str = "update", fork: str = 
     b.n = n
     b.npool = 0
     src = buf if buf.size else np.zeros(1, np.uint8)
-    rc = _lib(lib).lcv_ssz_decode_updates(ptr(src), ptr(offs, C.c_uint64), ptr(lens, C.c_uint64), n, KINDS[kind],
-                                         FORKS[fork], C.byref(b), ptr(pool_src, C.c_uint64), C.byref(npool),
-                                         ptr(status))
+    if forks is None:
+        rc = _lib(lib).lcv_ssz_decode_updates(ptr(src), ptr(offs, C.c_uint64), ptr(lens, C.c_uint64), n,
+                                             KINDS[kind], fcode, C.byref(b), ptr(pool_src, C.c_uint64),
+                                             C.byref(npool), ptr(status))
+    else:
+        fk = forks if forks.size else np.zeros(1, np.uint8)
+        rc = _lib(lib).lcv_ssz_decode_updates_mixed(ptr(src), ptr(offs, C.c_uint64), ptr(lens, C.c_uint64), n,
+                                                   KINDS[kind], ptr(fk), C.byref(b), ptr(pool_src, C.c_uint64),
+                                                   C.byref(npool), ptr(status))
     if rc != 0:
         raise ValueError(f"lcv_ssz_decode_updates: status {rc}")
     k = int(npool.value)
@@ -102,7 +140,7 @@ def decode_updates_status(messages: Messages, kind: str = "update", fork: str = 
     return batch, status[:n] == 0
 
 
-def decode_updates(messages: Messages, kind: str = "update", fork: str = "deneb",
+def decode_updates(messages: Messages, kind: str = "update", fork="deneb",
                    lib: Optional[Lib] = None) -> PackedUpdates:
     """Strict decode: raises ValueError (as upstream SSZ deserialisation does) if any message is malformed."""
     batch, ok = decode_updates_status(messages, kind, fork, lib)
@@ -146,6 +184,10 @@ _EXEC_SPANS = ((0, 32), (32, 52), (64, 96), (96, 128), (544, 800), (160, 192), (
 
 
 def _encode_header(beacon: np.ndarray, rec: np.ndarray, branch: np.ndarray, fork: str) -> bytes:
+    if fork == "altair":  # LightClientHeader = {beacon}: the execution data must be empty
+        if np.asarray(rec).any() or np.asarray(branch).any():
+            raise ValueError("an Altair-format header carries no execution data")
+        return np.asarray(beacon).tobytes()
     elen = int.from_bytes(rec[800:804].tobytes(), "little")
     spans = _EXEC_SPANS if fork == "deneb" else _EXEC_SPANS[:15]
     fixed = 584 if fork == "deneb" else 568
@@ -163,6 +205,16 @@ def encode_updates(batch: PackedUpdates, kind: str = "update", fork: str = "dene
     for i in range(batch.n):
         att = _encode_header(batch.att_beacon[i], batch.att_exec[i], batch.att_branch[i], fork)
         tail = batch.sync_bits[i].tobytes() + batch.sync_signature[i].tobytes() + int(batch.signature_slot[i]).to_bytes(8, "little")
+        if fork == "altair":  # every container fixed-size: fields in order, no offsets
+            fin = _encode_header(batch.fin_beacon[i], batch.fin_exec[i], batch.fin_branch[i], fork)
+            if kind == "optimistic":
+                out.append(att + tail)
+            elif kind == "finality":
+                out.append(att + fin + batch.finality_branch[i].tobytes() + tail)
+            else:
+                out.append(att + batch.nsc_pool[int(batch.nsc_index[i])].tobytes() + batch.nsc_branch[i].tobytes()
+                           + fin + batch.finality_branch[i].tobytes() + tail)
+            continue
         if kind == "optimistic":
             fixed = 4 + len(tail)
             out.append(fixed.to_bytes(4, "little") + tail + att)
@@ -188,5 +240,7 @@ def encode_bootstrap(beacon: bytes, execution: bytes, execution_branch: bytes, c
     if len(committee) != L.SYNC_COMMITTEE_BYTES or len(committee_branch) != 160:
         raise ValueError("committee must be 24,624 bytes and its branch 5 x 32 bytes")
     hdr = _encode_header(u8(beacon), u8(execution), u8(execution_branch), fork)
+    if fork == "altair":
+        return hdr + bytes(committee) + bytes(committee_branch)
     fixed = 4 + L.SYNC_COMMITTEE_BYTES + 160
     return fixed.to_bytes(4, "little") + bytes(committee) + bytes(committee_branch) + hdr

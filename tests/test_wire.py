@@ -271,3 +271,67 @@ def test_encode_reproduces_reference_bytes(kind):
     k = ["update", "finality", "optimistic"][kind]
     batch = wire.decode_updates(msgs, kind=k, lib=libs()[0])
     assert wire.encode_updates(batch, kind=k) == msgs
+
+
+class AltairHeader(Container):  # upstream altair LightClientHeader: beacon only (fixed-size)
+    beacon: S.BeaconBlockHeader
+
+
+class AltairUpdate(Container):
+    attested_header: AltairHeader
+    next_sync_committee: S.SyncCommittee
+    next_sync_committee_branch: S.NextSyncCommitteeBranch
+    finalized_header: AltairHeader
+    finality_branch: S.FinalityBranch
+    sync_aggregate: S.SyncAggregate
+    signature_slot: S.Slot
+
+
+def test_mixed_fork_response():
+    """A LightClientUpdatesByRange response straddling fork boundaries (per-chunk ForkDigest context,
+    p2p-interface.md:189-200): a Deneb, a Capella and an Altair-format chunk decoded in one pass with a
+    fork per message.  The Altair chunk is serialised by the oracle's SSZ from upstream altair
+    containers (not in the reference) and decodes to the golden row's Capella upgrade (empty execution);
+    encode_updates(fork="altair") reproduces the same bytes."""
+    from lcv.config import MAINNET, TESTNET
+    from lcv.device import PackedUpdates
+    w, g = load_wire(), load_updates()
+    p = PackedUpdates(nsc_pool=g["nsc_pool"], nsc_index=g["nsc_index"], signature_slot=g["signature_slot"],
+                      **{k: g[k] for k in COLS})
+    sel_deneb = [int(np.flatnonzero((w["kind"] == 0) & (w["row"] == 0))[0])]
+    u = H.update_from(p, 30)  # bellatrix_valid: pre-Capella, empty execution
+    alt = serialize(AltairUpdate(attested_header=AltairHeader(beacon=u.attested_header.beacon),
+                                 next_sync_committee=u.next_sync_committee,
+                                 next_sync_committee_branch=u.next_sync_committee_branch,
+                                 finalized_header=AltairHeader(beacon=u.finalized_header.beacon),
+                                 finality_branch=u.finality_branch, sync_aggregate=u.sync_aggregate,
+                                 signature_slot=u.signature_slot))
+    assert wire.encode_updates(p.slice(30, 31), "update", "altair")[0] == alt
+    cap = wire.encode_updates(p.slice(28, 29), "update", "capella")[0]
+    msgs = messages(w, sel_deneb) + [cap, alt]
+    rows = np.array([0, 28, 30])
+    exp, committees = expected_rows(g, rows, 0)
+    for lib in libs():
+        batch = wire.decode_updates(msgs, fork=["deneb", "capella", "altair"], lib=lib)
+        for k in COLS:
+            assert np.array_equal(getattr(batch, k), exp[k]), k
+        assert np.array_equal(batch.nsc_pool[batch.nsc_index], committees)
+        # the fork decides the layout: the Altair chunk under the Capella layout is malformed
+        _, ok = wire.decode_updates_status(msgs, fork=["deneb", "capella", "capella"], lib=lib)
+        assert list(ok) == [True, True, False]
+    # the finality / optimistic Altair forms and the bootstrap round-trip too
+    for kind in ("finality", "optimistic"):
+        m = wire.encode_updates(p.slice(30, 31), kind, "altair")
+        b = wire.decode_updates(m, kind=kind, fork="altair")
+        assert wire.encode_updates(b, kind, "altair") == m
+    bt = wire.encode_bootstrap(p.att_beacon[30], p.att_exec[30], p.att_branch[30], g["nsc_pool"][0].tobytes(),
+                               bytes(range(160)), fork="altair")
+    d = wire.decode_bootstrap(bt, fork="altair")
+    assert d.beacon.tobytes() == p.att_beacon[30].tobytes() and not d.execution.any()
+    assert d.current_sync_committee_branch.tobytes() == bytes(range(160))
+    # ForkDigest context -> container namespace, under the network configuration
+    assert wire.fork_of_digest_version(MAINNET.BELLATRIX_FORK_VERSION, MAINNET) == "altair"
+    assert wire.fork_of_digest_version(MAINNET.CAPELLA_FORK_VERSION, MAINNET) == "capella"
+    assert wire.fork_of_digest_version(TESTNET.DENEB_FORK_VERSION, TESTNET) == "deneb"
+    with pytest.raises(ValueError):
+        wire.fork_of_digest_version(MAINNET.GENESIS_FORK_VERSION, MAINNET)
