@@ -170,6 +170,10 @@ def main():
             comm.close()
         return
     wire_out = wire_path(v, sb, args.n)
+    try:
+        latency = latency_lines(v, sb)
+    except Exception as e:  # reported, never fatal to the throughput measurement
+        latency = {"error": repr(e)}
     total = world * args.n * args.steps
     stage_avg = {k: round(ms / args.steps, 3) for k, ms in stage_ms.items() if ms > 0}
     kernel_ms = sum(stage_avg.values())
@@ -208,6 +212,7 @@ def main():
         "roofline": roof,
         "configs": configs,
         "wire": wire_out,
+        "latency": latency,
     }
     if not args.no_cpu_baseline and world == 1:
         try:
@@ -217,6 +222,38 @@ def main():
     print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
+
+
+def latency_lines(v, sb, calls: int = 20) -> dict:
+    """Single-call latency of the reference-shaped drop-ins (the per-update usage at sync-protocol.md:512
+    and :464): one update validated against the resident store through the C ABI, and
+    FastAggregateVerify over the 512-key committee (first call decodes and KeyValidates the keys; later
+    calls with the same keys reuse the decoded table).  Medians over `calls` calls, ms."""
+    from lcv import synth
+    gvr = sb.genesis_validators_root
+    one = sb.updates.slice(0, 1)
+    v.validate(one, sb.current_slot, gvr)
+    ts = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        ok, _ = v.validate(one, sb.current_slot, gvr)
+        ts.append(time.perf_counter() - t0)
+    pks = [sb.current.pubkeys[48 * j:48 * j + 48] for j in range(512)]
+    msg = synth.signing_root(sb.updates.att_beacon[0].tobytes(), int(sb.updates.signature_slot[0]), gvr)
+    sig = sb.updates.sync_signature[0].tobytes()
+    pks_first = pks[1:] + pks[:1]  # a different table (order) than the later calls: a cold decode
+    t0 = time.perf_counter()
+    v.fast_aggregate_verify(pks_first, msg, sig)
+    first = time.perf_counter() - t0
+    fav_ok = v.fast_aggregate_verify(pks, msg, sig)
+    tf = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        fav_ok &= v.fast_aggregate_verify(pks, msg, sig)
+        tf.append(time.perf_counter() - t0)
+    return {"validate_one_update_ms": round(1000 * float(np.median(ts)), 3), "validate_one_update_valid": bool(ok[0]),
+            "fast_aggregate_verify_512_ms": round(1000 * float(np.median(tf)), 3),
+            "fast_aggregate_verify_512_cold_ms": round(1000 * first, 3), "fast_aggregate_verify_valid": bool(fav_ok)}
 
 
 def wire_path(v, sb, n: int) -> dict:
