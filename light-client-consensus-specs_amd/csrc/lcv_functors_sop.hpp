@@ -93,18 +93,21 @@ struct F_sop_acc {
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
   LCV_HD const uint32_t* io_in(uint32_t i) const { return W.lines + (size_t)i * SOP_LINE_WORDS; }
   LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
+  // lane l handles the Fp12 coefficients l, l + TEAM, ... (any team size)
   LCV_HD void prologue(uint32_t, uint32_t lane, uint32_t* lds) const {  // f = 1
-    if (lane >= 12) return;
-    fp x;
-    if (lane == 0) fp_one(x);
-    else fp_zero(x);
-    LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * lane + j] = x.v[j];
+    for (uint32_t s = lane; s < 12; s += TEAM) {
+      fp x;
+      if (s == 0) fp_one(x);
+      else fp_zero(x);
+      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * s + j] = x.v[j];
+    }
   }
   LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {  // slot 2g + c -> W.f
-    if (lane >= 12) return;
-    fp x;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = lds[12 * lane + j];
-    soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), x);
+    for (uint32_t s = lane; s < 12; s += TEAM) {
+      fp x;
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = lds[12 * s + j];
+      soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(s >> 1) + (s & 1u), x);
+    }
   }
 };
 
@@ -117,20 +120,23 @@ struct F_sop_fexp {
   LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
   LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
   LCV_HD void prologue(uint32_t i, uint32_t lane, uint32_t* lds) const {
-    if (lane >= 12) return;
-    fp x;
-    soa_ld_fp(x, W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u));
-    LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * lane + j] = x.v[j];
+    for (uint32_t s = lane; s < 12; s += TEAM) {
+      fp x;
+      soa_ld_fp(x, W.f, W.cap, i, 2 * fp12_soa_slot(s >> 1) + (s & 1u));
+      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * s + j] = x.v[j];
+    }
   }
   // the pairing value (e^3) to W.f; "== 1" to W.pair_ok
   LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {
-    if (lane >= 12) return;
     const uint32_t* r = lds + 12 * LCV_SOP_FEXP_SLOT_R0_0;
-    fp x;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = r[12 * lane + j];
-    soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(lane >> 1) + (lane & 1u), x);
+    for (uint32_t s = lane; s < 12; s += TEAM) {
+      fp x;
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = r[12 * s + j];
+      soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(s >> 1) + (s & 1u), x);
+    }
     if (lane == 0) {
-      fp one;
+      fp x, one;
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = r[j];
       fp_one(one);
       bool ok = fp_eq(x, one);
       for (uint32_t k = 1; k < 12; ++k) {

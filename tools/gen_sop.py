@@ -46,6 +46,7 @@ ACC_BITS = 800                     # 25 x 32-bit accumulator words
 MAXK = 15
 SLOT_MASK = 0xFFF
 NEG = 0x8000                       # term halfword: slot | NEG
+SHADOW_NONE = 0x3FF                # record word 1: no shadow slot
 
 
 def mont(x):
@@ -82,6 +83,8 @@ class Op:
         self.kind = kind
         self.load = load    # (ld_slot, io index): side-load of an Fp value from the program's input stream
         self.emit = emit    # io index: the result is also written to the program's output stream
+        self.dst_shadow = None   # slot that also receives p - result (Program.apply_shadows)
+        self.load_shadow = None  # slot that also receives p - loaded value
         for x, y, m in self.prods:
             assert 1 <= len(x) <= 2 and 1 <= len(y) <= 2 and m != 0
         assert len(self.adds) <= 2
@@ -151,8 +154,91 @@ class Program:
         assert split is not None, f"{self.name}: split round reads a slot an earlier part wrote"
         self.rounds.extend(split)
 
+    # ------------------------------------------------------------ negated shadows
+    def apply_shadows(self):
+        """Remove every negated product-operand read.  A product term -v (read as p - v) costs each lane
+        a 12-word subtraction and select per term in every round with any negation (the header's
+        flag is wave-uniform), which measured as ~45% of a K = 4 op (tools/microbench/sopbench.hip).
+        Instead, the op that produces v (or the round that side-loads it) also stores p - v in a
+        shadow slot, once, and the readers read that slot.  Negated constants become constants
+        p - c.  Values the program does not produce (the prologue's inputs) get their shadows from
+        one extra first round of add-in ops (dst = R * (-1) * v).  Shadow slots are allocated above
+        the program's slots by interval colouring over each shadow's live range (written at the end
+        of its round, last read in a later round: a slot whose old shadow is last read in round r
+        may take a new shadow written in round r, since a round's reads precede its stores)."""
+        if getattr(self, "_shadowed", False):
+            return
+        self._shadowed = True
+        producer = {}          # slot -> current value id
+        need = {}              # value id -> last round (in the final numbering) that reads -v
+        reads = []             # (round index, op, kind, k, j, value id) for rewriting
+        inputs = []            # value ids of prologue inputs
+        for r, ops in enumerate(self.rounds):
+            for o in ops:
+                for k, (x, y, m) in enumerate(o.prods):
+                    for kind, terms in (("x", x), ("y", y)):
+                        for j, t in enumerate(terms):
+                            if not t.neg:
+                                continue
+                            if isinstance(t.slot, tuple):  # constant: use the constant p - c
+                                terms[j] = T(self.const(P - self.const_list_value(t.slot)))
+                                continue
+                            vid = producer.get(t.slot)
+                            if vid is None:
+                                vid = producer[t.slot] = ("input", t.slot)
+                                inputs.append(vid)
+                            need[vid] = r
+                            reads.append((r, o, kind, k, j, vid))
+            for lane, o in enumerate(ops):   # the round's stores follow its reads
+                producer[o.dst] = ("op", r, lane)
+                if o.load:
+                    producer[o.load[0]] = ("load", r, lane)
+        # prologue inputs: one extra first round (indices of later rounds shift by one)
+        shift = 1 if inputs else 0
+        starts = {}
+        for vid in need:
+            starts[vid] = 0 if vid[0] == "input" else vid[1] + shift
+        for vid in list(need):
+            need[vid] += shift
+        # interval colouring: value live (start, end]; slot free for a new value starting at t if the
+        # previous value's end <= t
+        order = sorted(need, key=lambda v: (starts[v], need[v]))
+        slot_end = []          # per shadow slot: the end of its current value
+        shadow = {}
+        for vid in order:
+            st, en = starts[vid], need[vid]
+            for k, e in enumerate(slot_end):
+                if e <= st:
+                    slot_end[k] = en
+                    shadow[vid] = self.nslots + k
+                    break
+            else:
+                shadow[vid] = self.nslots + len(slot_end)
+                slot_end.append(en)
+        self.nshadow = len(slot_end)
+        for r, o, kind, k, j, vid in reads:
+            x, y, m = o.prods[k]
+            (x if kind == "x" else y)[j] = T(shadow[vid])
+        for vid, sh in shadow.items():
+            if vid[0] == "op":
+                self.rounds[vid[1]][vid[2]].dst_shadow = sh
+            elif vid[0] == "load":
+                self.rounds[vid[1]][vid[2]].load_shadow = sh
+        if inputs:
+            ops = [Op(shadow[v], [], [(v[1], -1)]) for v in inputs]
+            self.rounds[:0] = [ops[i:i + self.team] for i in range(0, len(ops), self.team)]
+            assert len(ops) <= self.team, "more prologue inputs to negate than lanes"
+        self.nslots += self.nshadow
+
+    def const_list_value(self, c):
+        for v, k in self.consts.items():
+            if k == c[1]:
+                return v
+        raise KeyError(c)
+
     # ------------------------------------------------------------ finalise: slot numbers of constants
     def finalize(self):
+        self.apply_shadows()
         if 0 not in self.consts:
             self.consts[0] = len(self.consts)
         self.base_const = self.nslots
@@ -192,10 +278,11 @@ class Program:
     def encode(self):
         """hdr: 4 u32 per round (wave-uniform):
              w0 = K | nadd << 4 | mflag << 6 | x2 << 7 | y2 << 8 | neg << 9 | inv << 10 | load << 11 |
-                  emit << 12 | red << 16 | used << 24
+                  emit << 12 | shadow << 13 | red << 16 | used << 24
              w1 = record offset (u32 words), w2 = record words per lane, w3 = 0
            rec: per lane (T lanes per round; lanes >= used: dst = SLOT_NONE):
-             r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;  r1 = io index;
+             r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;
+             r1 = io index | dst_shadow << 12 | load_shadow << 22  (shadow slots 10 bits, 0x3FF = none);
              r2, r3 = add-in term: slot | coef << 16 (signed 16-bit);  then per product k:
              [x0 | x1 << 16], [y0 | y1 << 16], [m]    (term = slot | NEG; padding = zero const)"""
         self.finalize()
@@ -212,10 +299,12 @@ class Program:
             inv = any(o.kind == "inv" for o in ops)
             load = any(o.load for o in ops)
             emit = any(o.emit is not None for o in ops)
+            shadow = any(o.dst_shadow is not None or o.load_shadow is not None for o in ops)
             red = max(self.red_steps(o) for o in ops)
             words = 4 + 3 * K
             hdr += [K | nadd << 4 | int(mflag) << 6 | int(x2) << 7 | int(y2) << 8 | int(neg) << 9 | int(inv) << 10 |
-                    int(load) << 11 | int(emit) << 12 | red << 16 | len(ops) << 24, len(rec), words, 0]
+                    int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | red << 16 | len(ops) << 24,
+                    len(rec), words, 0]
             for lane in range(self.team):
                 w = [0] * words
                 if lane >= len(ops):
@@ -228,7 +317,12 @@ class Program:
                 o = ops[lane]
                 flags = (1 if o.kind == "inv" else 0) | (2 if o.load else 0) | (4 if o.emit is not None else 0)
                 w[0] = self.sl(o.dst) | flags << 12 | ((self.sl(o.load[0]) if o.load else 0) << 16)
-                w[1] = (o.load[1] if o.load else o.emit if o.emit is not None else 0)
+                io = (o.load[1] if o.load else o.emit if o.emit is not None else 0)
+                assert 0 <= io < 4096
+                ds = SHADOW_NONE if o.dst_shadow is None else o.dst_shadow
+                ls = SHADOW_NONE if o.load_shadow is None else o.load_shadow
+                assert ds <= SHADOW_NONE and ls <= SHADOW_NONE
+                w[1] = io | ds << 12 | ls << 22
                 assert not (o.load and o.emit is not None)
                 for j in range(2):
                     if j < len(o.adds):
@@ -273,7 +367,7 @@ class Program:
                 def term(h):
                     s = h & SLOT_MASK
                     v = mem[s]
-                    assert 0 <= v < P
+                    assert 0 <= v <= P   # a shadow slot holds p - v in (0, p]
                     return (P - v) if h & NEG else v
                 acc = 0
                 for k in range(K):
@@ -290,6 +384,7 @@ class Program:
                     s, c = w[2 + j] & SLOT_MASK, w[2 + j] >> 16
                     c = c - 65536 if c >= 32768 else c
                     v = mem[s]
+                    assert 0 <= v <= P
                     acc += R * (abs(c) * ((P - v) if c < 0 else v))
                 assert acc < (1 << ACC_BITS)
                 m_ = (acc % R) * NP % R
@@ -299,13 +394,19 @@ class Program:
                         res -= P << s_
                 assert res < P, (self.name, r, lane)
                 flags = (w[0] >> 12) & 7
+                io, dsh, lsh = w[1] & 0xFFF, (w[1] >> 12) & SHADOW_NONE, (w[1] >> 22) & SHADOW_NONE
+                shadow = (w0 >> 13) & 1
                 if flags & 1:  # inversion of the add-in value (its first term)
                     res = mont(pow(unmont(res), P - 2, P)) if res else 0
                 if flags & 2:
-                    writes.append((w[0] >> 16, io_in[w[1]]))
+                    writes.append(((w[0] >> 16) & SLOT_MASK, io_in[io]))
+                    if shadow and lsh != SHADOW_NONE:
+                        writes.append((lsh, P - io_in[io]))
                 if flags & 4:
-                    io_out[w[1]] = res
+                    io_out[io] = res
                 writes.append((dst, res))
+                if shadow and dsh != SHADOW_NONE:
+                    writes.append((dsh, P - res))
             for s, v in writes:
                 mem[s] = v
         return mem
