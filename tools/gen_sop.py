@@ -296,6 +296,7 @@ class Program:
             x2 = any(len(x) == 2 for o in ops for x, _, _ in o.prods)
             y2 = any(len(y) == 2 for o in ops for _, y, _ in o.prods)
             neg = any(t.neg for o in ops for x, y, _ in o.prods for t in x + y)
+            assert not neg, "a negated product term survived apply_shadows (the device has no run-time path)"
             inv = any(o.kind == "inv" for o in ops)
             load = any(o.load for o in ops)
             emit = any(o.emit is not None for o in ops)
