@@ -30,8 +30,8 @@ struct Shape { const char* name; int K, x2, y2, neg, mflag; };
 
 int main() {
   Shape shapes[] = {{"K1 plain", 1, 0, 0, 0, 0}, {"K4 plain", 4, 0, 0, 0, 0}, {"K7 plain", 7, 0, 0, 0, 0},
-                    {"K4 +neg", 4, 0, 0, 1, 0}, {"K4 +x2y2", 4, 1, 1, 0, 0}, {"K4 +x2y2+neg", 4, 1, 1, 1, 0},
-                    {"K4 +x2y2+neg+m", 4, 1, 1, 1, 1}, {"K4 +m", 4, 0, 0, 0, 1}};
+                    {"K4 +x2", 4, 1, 0, 0, 0}, {"K4 +x2y2", 4, 1, 1, 0, 0}, {"K4 +x2y2+m", 4, 1, 1, 0, 1},
+                    {"K4 +m", 4, 0, 0, 0, 1}};
   uint32_t *drec, *dout;
   hipMalloc(&drec, 4096);
   hipMalloc(&dout, 4096 * 64 * 4);
