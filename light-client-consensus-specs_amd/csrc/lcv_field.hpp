@@ -379,72 +379,162 @@ LCV_FN void fp_from_be48_mont(fp& r, const uint8_t* p) {  // caller guarantees v
   fp_to_mont(r, raw);
 }
 
-// Variable-time binary extended Euclid on canonical values: r = a^-1 mod p (0 -> 0).  Verification
-// handles public data only, so variable time is acceptable; it is ~10x fewer cycles than a^(p-2).
-LCV_FN bool raw_is_one(const fp& a) {
-  uint32_t x = a.v[0] ^ 1u;
-  LCV_UNROLL for (int i = 1; i < 12; ++i) x |= a.v[i];
-  return x == 0;
-}
-LCV_FN void raw_shr1(fp& a) {
-  LCV_UNROLL for (int j = 0; j < 11; ++j) a.v[j] = (a.v[j] >> 1) | (a.v[j + 1] << 31);
-  a.v[11] >>= 1;
-}
-LCV_FN bool raw_sub(fp& r, const fp& a, const fp& b) {  // r = a - b, returns borrow
-  uint32_t br = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = subc32(a.v[j], b.v[j], br, br);
-  return br != 0;
-}
-LCV_FN void raw_half_mod(fp& x) {  // x / 2 mod p, x < p
-  constexpr uint32_t PL[12] = LCV_P_INIT;
-  const uint32_t m = 0u - (x.v[0] & 1u);
-  uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = addc32(x.v[j], PL[j] & m, c, c);
-  raw_shr1(x);  // x + p < 2^382: no bit is lost
-}
-LCV_FN void raw_sub_mod(fp& r, const fp& a, const fp& b) {  // (a - b) mod p, a, b < p
-  constexpr uint32_t PL[12] = LCV_P_INIT;
-  const uint32_t m = raw_sub(r, a, b) ? 0xFFFFFFFFu : 0u;
-  uint32_t c = 0;
-  LCV_UNROLL for (int j = 0; j < 12; ++j) r.v[j] = addc32(r.v[j], PL[j] & m, c, c);
-}
-LCV_FN void fp_inv_bingcd(fp& r, const fp& a_mont) {
-  fp u, v, x1, x2, t;
-  fp_from_mont(u, a_mont);
-  if (fp_is_zero(u)) {
-    fp_zero(r);
-    return;
+// ---- Bernstein-Yang "safegcd" inversion, variable time (Bernstein & Yang, "Fast constant-time gcd
+// computation and modular inversion", TCHES 2019; batching of the var-time divsteps as described in
+// libsecp256k1's doc/safegcd_implementation.md).  Values are 13 signed 30-bit limbs (limbs 0..11 in
+// [0, 2^30), limb 12 signed).  Each batch runs 30 divsteps on the low words of f, g only, giving a
+// 2x2 matrix (u v; q r) with |u| + |v| <= 2^30, then applies it to the full f, g (exact division by
+// 2^30) and to the Bezout coefficients d, e modulo p.  Invariants: f = d a, g = e a (mod p); the loop
+// ends at g = 0 with f = +-1, so a^-1 = +-d.  Every lane runs the same instruction stream except the
+// short divstep loop: ~30 batches instead of round 1's ~760 branchy shift/subtract steps of a binary
+// extended Euclid (tools/microbench/soptrace.hip: that SOP inversion round took 0.4 ms per 10^4 items).
+struct s30 { int32_t v[13]; };
+constexpr int32_t kM30 = 0x3FFFFFFF;
+
+// 30 divsteps on (eta = -delta, f0, g0): returns eta, t = (u, v, q, r) with
+// [f'; g'] 2^30 = t [f; g]  (f odd throughout; the steps that only halve g run at once via ctz,
+// the additions of f to odd g cancel up to min(eta + 1, remaining, 12) low bits at once)
+LCV_FN int32_t by_divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  int i = 30;
+  for (;;) {
+    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {  // delta > 0 and g odd: (f, g) <- (g, -f)
+      uint32_t tmp;
+      eta = -eta;
+      tmp = f; f = g; g = 0u - tmp;
+      tmp = u; u = q; q = 0u - tmp;
+      tmp = v; v = r; r = 0u - tmp;
+    }
+    const int limit = (eta + 1) > i ? i : (eta + 1);
+    const uint32_t m = (0xFFFFFFFFu >> (32 - limit)) & 0xFFFu;
+    uint32_t x = f;                 // f^-1 mod 2^12 by Newton (f odd: f * f = 1 mod 8)
+    x *= 2u - f * x;
+    x *= 2u - f * x;
+    const uint32_t w = (0u - g * x) & m;  // g + w f = 0 mod 2^min(limit, 12)
+    g += f * w;
+    q += u * w;
+    r += v * w;
   }
-  LCV_FP_SET(v, LCV_P_INIT);
-  fp_zero(x1);
-  x1.v[0] = 1;
-  fp_zero(x2);
-  while (!raw_is_one(u) && !raw_is_one(v)) {
-    // op counter: each shift + modular halving, and each subtraction pair, is two Fp additions' work
-    while ((u.v[0] & 1u) == 0) {
-      LCV_COUNT(1); LCV_COUNT(1);
-      raw_shr1(u);
-      raw_half_mod(x1);
-    }
-    while ((v.v[0] & 1u) == 0) {
-      LCV_COUNT(1); LCV_COUNT(1);
-      raw_shr1(v);
-      raw_half_mod(x2);
-    }
-    LCV_COUNT(1); LCV_COUNT(1);
-    if (!raw_sub(t, u, v)) {  // u >= v
-      u = t;
-      raw_sub_mod(x1, x1, x2);
-    } else {
-      raw_sub(v, v, u);
-      raw_sub_mod(x2, x2, x1);
-    }
-  }
-  fp_to_mont(r, raw_is_one(u) ? x1 : x2);
+  t[0] = (int32_t)u; t[1] = (int32_t)v; t[2] = (int32_t)q; t[3] = (int32_t)r;
+  return eta;
 }
 
-// Fp inversion (inv0: 0 -> 0) for every stage: the binary algorithm above
-LCV_FN void fp_inv(fp& r, const fp& a) { fp_inv_bingcd(r, a); }
+// [d; e] <- (t [d; e] + p [md; me]) / 2^30, md / me chosen so the low 30 bits vanish; d, e stay in
+// (-2p, p) (md / me also add p when the input is negative)
+LCV_FN void by_update_de(s30& d, s30& e, const int32_t t[4]) {
+  constexpr int32_t PS[13] = LCV_P_S30_INIT;
+  const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
+  const int32_t sd = d.v[12] >> 31, se = e.v[12] >> 31;
+  int32_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
+  int64_t cd = (int64_t)u * d.v[0] + (int64_t)v * e.v[0];
+  int64_t ce = (int64_t)q * d.v[0] + (int64_t)r * e.v[0];
+  md -= (int32_t)((LCV_PINV30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)kM30);
+  me -= (int32_t)((LCV_PINV30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)kM30);
+  cd += (int64_t)PS[0] * md;
+  ce += (int64_t)PS[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+  LCV_UNROLL for (int k = 1; k < 13; ++k) {
+    const int32_t dk = d.v[k], ek = e.v[k];
+    cd += (int64_t)u * dk + (int64_t)v * ek + (int64_t)PS[k] * md;
+    ce += (int64_t)q * dk + (int64_t)r * ek + (int64_t)PS[k] * me;
+    d.v[k - 1] = (int32_t)cd & kM30;
+    cd >>= 30;
+    e.v[k - 1] = (int32_t)ce & kM30;
+    ce >>= 30;
+  }
+  d.v[12] = (int32_t)cd;
+  e.v[12] = (int32_t)ce;
+}
+
+// [f; g] <- t [f; g] / 2^30 (exact)
+LCV_FN void by_update_fg(s30& f, s30& g, const int32_t t[4]) {
+  const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
+  int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
+  int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
+  cf >>= 30;
+  cg >>= 30;
+  LCV_UNROLL for (int k = 1; k < 13; ++k) {
+    const int32_t fk = f.v[k], gk = g.v[k];
+    cf += (int64_t)u * fk + (int64_t)v * gk;
+    cg += (int64_t)q * fk + (int64_t)r * gk;
+    f.v[k - 1] = (int32_t)cf & kM30;
+    cf >>= 30;
+    g.v[k - 1] = (int32_t)cg & kM30;
+    cg >>= 30;
+  }
+  f.v[12] = (int32_t)cf;
+  g.v[12] = (int32_t)cg;
+}
+
+LCV_FN void fp_inv_by(fp& r, const fp& a_mont) {
+  constexpr int32_t PS[13] = LCV_P_S30_INIT;
+  constexpr uint32_t PL[12] = LCV_P_INIT;
+  s30 f, g, d, e;
+  // g = the Montgomery representative a R (< p), 30 bits per limb
+  LCV_UNROLL for (int k = 0; k < 13; ++k) {
+    const int b = 30 * k, w = b >> 5, s = b & 31;
+    uint32_t x = a_mont.v[w] >> s;
+    if (s > 2 && w + 1 < 12) x |= a_mont.v[w + 1] << (32 - s);
+    g.v[k] = (int32_t)(x & (uint32_t)kM30);
+    f.v[k] = PS[k];
+    d.v[k] = 0;
+    e.v[k] = 0;
+  }
+  e.v[0] = 1;
+  int32_t eta = -1;
+  // <= 1101 divsteps for 381-bit inputs (BY Theorem 11.2: floor((49 d + 57) / 17)), i.e. <= 37 batches
+  LCV_NOUNROLL for (int it = 0; it < 40; ++it) {
+    LCV_COUNT(1); LCV_COUNT(1); LCV_COUNT(1); LCV_COUNT(1);  // op counter: four 13-limb linear combinations
+    int32_t t[4];
+    eta = by_divsteps30(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    by_update_de(d, e, t);
+    by_update_fg(f, g, t);
+    int32_t z = 0;
+    LCV_UNROLL for (int k = 0; k < 13; ++k) z |= g.v[k];
+    if (z == 0) break;
+  }
+  // d in (-2p, p) as a 13-word two's complement integer; limbs 0..11 fill bits 0..359 exactly
+  uint32_t x[13];
+  LCV_UNROLL for (int w = 0; w < 13; ++w) x[w] = 0;
+  LCV_UNROLL for (int k = 0; k < 12; ++k) {
+    const int b = 30 * k, w = b >> 5, s = b & 31;
+    x[w] |= (uint32_t)d.v[k] << s;
+    if (s > 2) x[w + 1] |= (uint32_t)d.v[k] >> (32 - s);
+  }
+  x[11] |= (uint32_t)d.v[12] << 8;
+  x[12] = (uint32_t)(d.v[12] >> 24);
+  LCV_UNROLL for (int pass = 0; pass < 2; ++pass) {  // + p while negative
+    const uint32_t m = 0u - (x[12] >> 31);
+    uint32_t c = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) x[j] = addc32(x[j], PL[j] & m, c, c);
+    x[12] = x[12] + c;
+  }
+  // a^-1 = f d with f = +-1 (limb 12 of f is 0 or -1): p - d for f = -1 (d != 0)
+  uint32_t nz = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) nz |= x[j];
+  const uint32_t neg = (f.v[12] < 0 && nz != 0) ? 0xFFFFFFFFu : 0u;
+  fp y;
+  uint32_t br = 0;
+  LCV_UNROLL for (int j = 0; j < 12; ++j) {
+    const uint32_t n = subc32(PL[j], x[j], br, br);
+    y.v[j] = neg ? n : x[j];
+  }
+  // y = (a R)^-1  ->  a^-1 R = y R^3 R^-1
+  fp r3;
+  LCV_FP_SET(r3, LCV_R3_INIT);
+  fp_mul(r, y, r3);
+}
+
+// Fp inversion (inv0: 0 -> 0) for every stage: Bernstein-Yang above
+LCV_FN void fp_inv(fp& r, const fp& a) { fp_inv_by(r, a); }
 
 // ============================================================================ Fp2
 LCV_FN void fp2_zero(fp2& r) { fp_zero(r.c0); fp_zero(r.c1); }

@@ -58,7 +58,7 @@ def test_opcount_every_stage():
 
     def half_muls(p):
         return sum(len(o.prods) + 1 for r in p.rounds for o in r) / 2
-    assert per["final_exp"]["fp_mul"] == half_muls(fp) + 2  # + the inversion's Montgomery conversions
+    assert per["final_exp"]["fp_mul"] == half_muls(fp) + 1  # + the inversion's Montgomery correction (y R^3)
     assert per["miller_loop"]["fp_mul"] == half_muls(ap)
     assert per["miller_lines"]["fp_mul"] == half_muls(lp) == per["miller_lines_sig"]["fp_mul"]
     tot = c["total_per_update"]
@@ -74,3 +74,16 @@ def test_windowed_pow_hostsim(sim_verifier):
         b = out[i].tobytes()
         assert int.from_bytes(b[:48], "big") == pow(x, (P + 1) // 4, P)
         assert int.from_bytes(b[48:], "big") == pow(x, (P - 3) // 4, P)
+
+
+def test_fp_inverse_hostsim(sim_verifier):
+    """Bernstein-Yang inversion (lcv_field.hpp fp_inv_by) against pow(a, p - 2, p): 0 (inv0), 1, p - 1,
+    powers of two and p minus powers of two (long runs of equal bits), limb-boundary values, random."""
+    rng = np.random.default_rng(6)
+    xs = [0, 1, 2, 3, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, (1 << 30) - 1, 1 << 30, 1 << 32, (1 << 360) - 1]
+    xs += [(1 << k) % P for k in range(0, 384, 11)] + [P - (1 << k) for k in range(0, 380, 17)]
+    xs += [int.from_bytes(rng.bytes(48), "big") % P for _ in range(400)]
+    a = np.frombuffer(b"".join(x.to_bytes(48, "big") for x in xs), np.uint8)
+    out, _ = sim_verifier.debug_fp(a, a)
+    for i, x in enumerate(xs):
+        assert int.from_bytes(out[i].tobytes()[144:192], "big") == pow(x, P - 2, P), hex(x)
