@@ -295,7 +295,7 @@ STAGE_KERNELS = {"miller_lines": "k_sop<F_sop_lines>", "miller_lines_sig": "k_so
                  "final_exp": "k_sop<F_sop_fexp>",
                  "hash_to_g2": "k_sop<F_sop_h2c>", "h2c_sswu": "k_items<F_h2c_map>",
                  "sig_decode": "k_items<F_sig>",
-                 "g1_aggregate": "k_items<F_agg>", "pre_checks": "k_items<F_pre>",
+                 "g1_aggregate": "k_items<F_agg>", "pre_checks": "k_items<F_pre>", "signing_root": "k_items<F_sigroot>",
                  "nsc_htr": "k_team<F_nsc_team>"}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 

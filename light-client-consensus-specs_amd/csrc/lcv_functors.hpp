@@ -13,6 +13,7 @@ struct F_nsc_team {
   LCV_HD void operator()(uint32_t j, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t*) const { item_nsc_team(j, lane, r, lds, B, C, W); }
 };
 struct F_pre { BatchDev B; CommitteeDev C; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_pre(i, B, C, P, W); } };
+struct F_sigroot { BatchDev B; Params P; Work W; LCV_HD void operator()(uint32_t i) const { item_sigroot(i, B, P, W); } };
 struct F_h2c_map { Work W; LCV_HD void operator()(uint32_t t) const { item_h2c_map(t, W); } };
 struct F_sig { BatchDev B; Work W; LCV_HD void operator()(uint32_t i) const { item_sig(i, B, W); } };
 struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32_t i) const { item_agg(i, B, C, W); } };

@@ -8,7 +8,8 @@
 //
 // Stage map onto the reference's validate_light_client_update (sync-protocol.md:386-465):
 //   item_nsc_team   hash_tree_root(next_sync_committee) + default / store-equality tests (:439-449)
-//   item_pre        every non-BLS assert (:392-449) + signing root (:460-463) -> first failing reason
+//   item_pre        every non-BLS assert (:392-449) -> first failing reason, committee id
+//   item_sigroot    signing root (:460-463) -> W.msg
 //   item_h2c_map + SOP h2c program   hash_to_G2(signing_root)                  -+
 //   item_sig + SOP line walk          signature decode + G2 subgroup check      |  bls.FastAggregate-
 //   item_agg                          masked G1 aggregation of participant keys |  Verify (:464)
@@ -240,13 +241,20 @@ LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
     if (!merkle_branch_ok(leaf, nbr, 5, 23, state_root)) LCV_FAIL(13);
   }
 #undef LCV_FAIL
-  // :452-463 committee selection and signing root
+  // :452-459 committee selection (the signing root is item_sigroot's)
   W.comm_id[i] = sig_period != store_period ? 1u : 0u;
+  W.pre_reason[i] = (uint8_t)reason;
+}
+
+// :460-463 fork version, domain and signing root of the attested header -> W.msg.  A kernel of its own
+// (~10 SHA-256 compressions per update against item_pre's ~170), so hash_to_G2 starts without waiting
+// for the branch checks, which run beside it on another stream.
+LCV_FN void item_sigroot(uint32_t i, const BatchDev& B, const Params& P, const Work& W) {
+  const uint8_t* ab = B.att_beacon + (size_t)K_BEACON * i;
   h256 gvr, msg;
   LCV_UNROLL for (int k = 0; k < 8; ++k) gvr.w[k] = P.gvr[k];
-  signing_root(msg, ab, sig_slot, gvr, P.cfg);
+  signing_root(msg, ab, B.sig_slot[i], gvr, P.cfg);
   soa_st_h256(W.msg, W.cap, i, msg);
-  W.pre_reason[i] = (uint8_t)reason;
 }
 
 // ============================================================================ BLS stages

@@ -26,7 +26,8 @@ struct Prog {
 template <uint32_t T>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_trace(lcv::SopView P, uint32_t n,
                                                                                       uint32_t lds_words, uint32_t* io,
-                                                                                      uint32_t io_words, uint64_t* trace) {
+                                                                                      uint32_t io_words, uint64_t* trace,
+                                                                                      uint32_t* hwid) {
   constexpr uint32_t G = 64 / T;
   extern __shared__ uint32_t lds[];
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
@@ -50,7 +51,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (active) lcv::sop_exec(h0, P.rec + off + lane * words, my, my, lds, P.nslots, io_item, io_item);
     __syncthreads();
   }
-  if (threadIdx.x == 0) tr[R] = wall_clock64();
+  if (threadIdx.x == 0) {
+    tr[R] = wall_clock64();
+    hwid[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);       // HW_ID: wave, SIMD, CU, SH, SE
+    hwid[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
 }
 
 template <uint32_t T>
@@ -71,13 +76,15 @@ void run(const Prog& pg) {
   uint64_t* trace;
   const size_t tn = (size_t)blocks * (pg.rounds + 1);
   hipMalloc(&trace, tn * 8);
+  uint32_t* hw;
+  hipMalloc(&hw, (size_t)blocks * 8);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  hipLaunchKernelGGL(k_trace<T>, dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace);
+  hipLaunchKernelGGL(k_trace<T>, dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace, hw);
   hipDeviceSynchronize();
   hipEventRecord(a);
-  hipLaunchKernelGGL(k_trace<T>, dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace);
+  hipLaunchKernelGGL(k_trace<T>, dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace, hw);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -91,8 +98,55 @@ void run(const Prog& pg) {
     for (uint32_t r = 0; r < pg.rounds; ++r) per[r] += (double)(tb[r + 1] - tb[r]) * 10.0 / blocks;  // ns
     span += (double)(tb[pg.rounds] - tb[0]) * 10.0 / blocks;
   }
-  printf("== %s: team %u, %u items, %u blocks, %u rounds: kernel %.3f ms, mean block round span %.3f ms\n",
-         pg.name, T, pg.items, blocks, pg.rounds, ms, span * 1e-6);
+  uint64_t s0 = ~0ull, s1 = 0, e0 = ~0ull, e1 = 0;
+  for (uint32_t bk = 0; bk < blocks; ++bk) {
+    const uint64_t* tb = t.data() + (size_t)bk * (pg.rounds + 1);
+    s0 = std::min(s0, tb[0]); s1 = std::max(s1, tb[0]);
+    e0 = std::min(e0, tb[pg.rounds]); e1 = std::max(e1, tb[pg.rounds]);
+  }
+  printf("== %s: team %u, %u items, %u blocks, %u rounds: kernel %.3f ms, mean block round span %.3f ms; "
+         "first round starts over %.3f ms, last rounds end over %.3f ms, first start to last end %.3f ms\n",
+         pg.name, T, pg.items, blocks, pg.rounds, ms, span * 1e-6, (s1 - s0) * 1e-5, (e1 - e0) * 1e-5,
+         (e1 - s0) * 1e-5);
+  {  // waves per SIMD (blocks are one wave) and the mean block span by that count
+    std::vector<uint32_t> h(2 * (size_t)blocks);
+    hipMemcpy(h.data(), hw, h.size() * 4, hipMemcpyDeviceToHost);
+    std::map<uint64_t, int> per_simd;
+    auto key = [&](uint32_t b) {
+      const uint32_t id = h[2 * b], x = h[2 * b + 1] & 15u;
+      const uint32_t simd = (id >> 4) & 3u, cu = (id >> 8) & 15u, sh = (id >> 12) & 1u, se = (id >> 13) & 7u;
+      return ((uint64_t)x << 24) | (se << 16) | (sh << 12) | (cu << 4) | simd;
+    };
+    for (uint32_t b = 0; b < blocks; ++b) per_simd[key(b)]++;
+    std::map<int, std::pair<int, double>> byw;
+    std::map<uint32_t, int> cus;
+    for (uint32_t b = 0; b < blocks; ++b) {
+      const uint64_t* tb = t.data() + (size_t)b * (pg.rounds + 1);
+      auto& e = byw[per_simd[key(b)]];
+      e.first++;
+      e.second += (double)(tb[pg.rounds] - tb[0]) * 1e-5;
+      cus[(uint32_t)(key(b) >> 4)]++;
+    }
+    std::map<uint32_t, std::pair<int, double>> byx;
+    std::vector<double> spans;
+    for (uint32_t b = 0; b < blocks; ++b) {
+      const uint64_t* tb = t.data() + (size_t)b * (pg.rounds + 1);
+      const double sp = (double)(tb[pg.rounds] - tb[0]) * 1e-5;
+      spans.push_back(sp);
+      auto& e = byx[(uint32_t)(key(b) >> 24)];
+      e.first++;
+      e.second += sp;
+    }
+    std::sort(spans.begin(), spans.end());
+    printf("  span percentiles (ms): p0 %.3f p10 %.3f p50 %.3f p90 %.3f p99 %.3f p100 %.3f; by XCC:", spans[0],
+           spans[spans.size() / 10], spans[spans.size() / 2], spans[spans.size() * 9 / 10], spans[spans.size() * 99 / 100],
+           spans.back());
+    for (auto& kv : byx) printf(" %u: %.3f", kv.first, kv.second.second / kv.second.first);
+    printf("\n");
+    printf("  %zu SIMDs and %zu CUs used;", per_simd.size(), cus.size());
+    for (auto& kv : byw) printf(" %d waves/SIMD: %d blocks, mean span %.3f ms;", kv.first, kv.second.first, kv.second.second / kv.second.first);
+    printf("\n");
+  }
   std::map<std::string, std::pair<int, double>> by;
   for (uint32_t r = 0; r < pg.rounds; ++r) {
     const uint32_t h0 = pg.hdr[4 * r];
@@ -120,6 +174,7 @@ void run(const Prog& pg) {
   printf("\n");
   hipFree(io);
   hipFree(trace);
+  hipFree(hw);
 }
 
 #define PROG(nm, N, items, iow)                                                                              \
