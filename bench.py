@@ -9,7 +9,14 @@ aggregation, Miller loop, final exponentiation, verdicts).  Inputs are resident 
 once, outside the timed region); for N > 1 each step ends with an RCCL all-gather of the per-rank
 verdict bytes (the only collective of the design).  Weak scaling: every rank owns `--n` updates.
 
+Default shape (--depth 2): the serving loop keeps two batches in flight — two resident batches of
+`--n` updates alternate over the two work-space slots of the context (lcv_validate_resident_async), so
+batch k+1's latency-bound early stages (SSWU, hash_to_G2) share the GPU with batch k's Miller loop and
+final exponentiation; each timed step is one whole batch, waited for and its verdicts read (or
+all-gathered) inside the timed region.  --depth 1 times one batch at a time; both rates are reported.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n UPDATES_PER_GPU] [--participation full|random]
+                    [--depth 1|2]
 """
 from __future__ import annotations
 
@@ -89,6 +96,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[2]/[3]/[4] lines")
     ap.add_argument("--pipeline", default="1,1", help="STREAMS,SLICES of the timed run (1,1 = serial stages)")
+    ap.add_argument("--depth", type=int, default=2, choices=[1, 2],
+                    help="batches in flight: 2 = double-buffered serving loop over two work-space slots "
+                         "(lcv_validate_resident_async), 1 = one batch at a time")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,6 +116,11 @@ def main():
     log(f"[rank {rank}] generated {args.n} updates in {time.perf_counter() - t0:.1f}s")
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     rb = v.upload(sb.updates)
+    # depth 2: a second, different batch of the same shape (same store), so the two slots alternate
+    # between two resident batches
+    sb2 = synth.generate(v, args.n, seed=1002 + rank, participation=args.participation) if args.depth == 2 else sb
+    rbs = [rb, v.upload(sb2.updates) if args.depth == 2 else rb]
+    sbs = [sb, sb2]
     pipe = tuple(int(x) for x in args.pipeline.split(","))
     v.set_pipeline(*pipe)
     verdict = np.zeros(args.n, np.uint8)
@@ -123,8 +138,34 @@ def main():
         if comm is not None:
             comm.barrier()
 
+    slot_ok = [True, True]
+    per_slot_v = [np.zeros(args.n, np.uint8), np.zeros(args.n, np.uint8)]
+    per_slot_r = [np.zeros(args.n, np.uint8), np.zeros(args.n, np.uint8)]
+    per_slot_g = [np.zeros(world * args.n, np.uint8), np.zeros(world * args.n, np.uint8)]
+
+    def collect(s):  # wait for slot s's batch; its verdicts (all-gathered over RCCL when N > 1)
+        if comm is None:
+            v.slot_wait(s, args.n, per_slot_v[s], per_slot_r[s])
+            slot_ok[s] = slot_ok[s] and bool((per_slot_v[s] == 1).all())
+        else:
+            comm.slot_allgather(s, args.n, args.n, per_slot_g[s])
+            slot_ok[s] = slot_ok[s] and bool((per_slot_g[s] == 1).all())
+
+    def stream_steps(k_steps):
+        # double-buffered serving loop: batch k runs in slot k % 2 while batch k - 1 is still on the GPU;
+        # the host waits for a slot (and reads its verdicts) only before reusing it, and drains both
+        for k in range(k_steps):
+            s = k % 2
+            if k >= 2:
+                collect(s)
+            v.validate_resident_async(rbs[s], sbs[s].current_slot, sbs[s].genesis_validators_root, s)
+        for k in range(max(0, k_steps - 2), k_steps):
+            collect(k % 2)
+
     for _ in range(args.warmup):
         step()
+    if args.depth == 2:
+        stream_steps(max(2, args.warmup))
     # correctness of what is timed: every synthetic update is valid
     if comm is None:
         v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
@@ -132,32 +173,41 @@ def main():
     else:
         step()
         ok_all = bool((gathered == 1).all())
-    serial = pipe == (1, 1)
+    serial = pipe == (1, 1) and args.depth == 1
     stage_ms = {k: 0.0 for k in v.last_timings()}
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        if serial:  # stage kernel times: HIP events on each stage's stream, inside the timed region
-            for k, ms in v.last_timings().items():
-                stage_ms[k] += ms
+    if args.depth == 2:
+        stream_steps(args.steps)
+    else:
+        for _ in range(args.steps):
+            step()
+            if serial:  # stage kernel times: HIP events on each stage's stream, inside the timed region
+                for k, ms in v.last_timings().items():
+                    stage_ms[k] += ms
     sync()
     dt = time.perf_counter() - t0
     if comm is not None:
         dt = comm.allreduce_max(dt)
+    if args.depth == 2:
+        ok_all = ok_all and all(slot_ok)
 
     serial_ms, serial_ok = 1000 * dt / args.steps, ok_all
     if not serial:
         # a multi-stream pipeline overlaps stages, so per-stage kernel times come from the serial
         # shape (no other kernel sharing the GPU), run after the timed region
         v.set_pipeline(1, 1)
+        sync()
         ts = time.perf_counter()
         for _ in range(args.steps):
-            v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
+            step()
             for k, ms in v.last_timings().items():
                 stage_ms[k] += ms
+        sync()
         serial_ms = 1000 * (time.perf_counter() - ts) / args.steps
-        serial_ok = bool((verdict == 1).all())
+        if comm is not None:
+            serial_ms = 1000 * comm.allreduce_max(serial_ms / 1000)
+        serial_ok = bool((verdict == 1).all()) if comm is None else bool((gathered == 1).all())
         v.set_pipeline(*pipe)
 
     # PCIe-inclusive rate (host batch -> device each time), reported beside `value`, never as it
@@ -201,13 +251,20 @@ def main():
                    "updates_per_gpu": args.n, "committee": 512, "parallelism": f"dp{world} (independent updates)"},
         "all_valid": ok_all and serial_ok,
         "pipeline": {"streams": pipe[0], "slices": pipe[1]},
+        "batches_in_flight": args.depth,
         "serial_ms_per_step": round(serial_ms, 3),
+        # one batch at a time (the latency-bound shape: every stage's launch waits for the previous)
+        "value_one_batch_at_a_time": round(world * args.n / (serial_ms / 1000), 1),
         # per-kernel HIP-event times (one mark per kernel); the signature chain runs on a second
         # stream beside the message chain, so their sum exceeds the wall time of a step
         "stage_kernel_ms_per_step": stage_avg,
         "sum_of_stage_kernel_ms": round(kernel_ms, 3),
-        "value_is": "kernel-only: inputs resident in HBM (uploaded once); pcie_inclusive_* copies the "
-                    "packed batch host->device and the verdicts back in every call",
+        "value_is": ("kernel-only: inputs resident in HBM (uploaded once); " +
+                     ("two batches in flight (double-buffered serving loop over two work-space slots, "
+                      "lcv_validate_resident_async): batch k+1's stages overlap batch k's, every batch's "
+                      "verdicts are waited for and copied out (all-gathered over RCCL for N > 1) inside the "
+                      "timed region; " if args.depth == 2 else "") +
+                     "pcie_inclusive_* copies the packed batch host->device and the verdicts back in every call"),
         "pcie_inclusive_updates_per_s_1gpu": round(pcie_rate, 1),
         "roofline": roof,
         "configs": configs,

@@ -120,6 +120,19 @@ int lcv_validate_resident(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot, co
 /* same, verdicts written to a DEVICE buffer of n bytes (for an RCCL all-gather); no host copy */
 int lcv_validate_resident_dev(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot,
                               const uint8_t* genesis_validators_root, uint8_t* verdict_dev);
+/* Two batches in flight (double-buffered serving loop; no reference counterpart: the reference
+ * validates one update per call, sync-protocol.md:386).  lcv_validate_resident_async enqueues the whole
+ * pipeline for b (at most 65536 updates) on the two HIP streams of work-space slot `slot` (0 or 1) and
+ * returns without waiting; lcv_slot_wait waits for that slot and copies the first n verdicts / reason
+ * codes out (either pointer may be NULL).  A slot's next batch starts on the device after its previous
+ * one; alternate the slots and wait for a slot before reading or reusing it. */
+int lcv_validate_resident_async(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot,
+                                const uint8_t* genesis_validators_root, int slot);
+int lcv_slot_wait(lcv_ctx* ctx, int slot, uint64_t n, uint8_t* verdict_out, uint8_t* reason_out);
+/* multi-GPU form of lcv_slot_wait: after slot `slot`'s batch (n <= per_rank rows), all-gather every rank's
+ * verdict bytes over RCCL (rank-major, each slice zero padded to per_rank) into verdict_all_out
+ * (nranks * per_rank bytes) and wait.  Collective: every rank calls it in the same order. */
+int lcv_slot_allgather(lcv_ctx* ctx, int slot, uint64_t n, uint64_t per_rank, uint8_t* verdict_all_out);
 /* Execution shape of lcv_validate_*: each 64k-update chunk is cut into `chunks` slices whose whole
  * stage chains run on min(streams, 4) HIP streams, so different slices' kernels overlap.  streams = 1
  * (default) runs the stages one after another over the whole chunk (per-stage timings available);

@@ -12,6 +12,7 @@
 #include <vector>
 
 #define LCV_HD __device__
+#include "lcv_common.hpp"  // LCV_SLOTS, EV_*
 
 struct lcv_ctx;
 
@@ -27,6 +28,8 @@ struct Backend {
   int open_stage[BE_STREAMS] = {-1, -1, -1, -1};
   hipEvent_t open_ev[BE_STREAMS] = {};
   hipEvent_t fork_ev[BE_STREAMS] = {}, join_ev[BE_STREAMS] = {};
+  int base = 0;                          // work-space slot s uses streams st[2s] (main), st[2s + 1] (side)
+  hipEvent_t ev[LCV_SLOTS][EV_COUNT] = {};  // run_bls's ordering events, per slot
   ncclComm_t comm = nullptr;  // RCCL communicator (lcv_comm_init), collectives on st[0]
   double* comm_scalar = nullptr;
 };
@@ -49,6 +52,10 @@ template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n
 static int be_fork(lcv_ctx* ctx);
 static int be_join(lcv_ctx* ctx);
 static void be_use_stream(lcv_ctx* ctx, int k);
+static void be_set_slot(lcv_ctx* ctx, int slot);
+static int be_mark(lcv_ctx* ctx, int ev, int k);
+static int be_wait(lcv_ctx* ctx, int k, int ev);
+static int be_sync_slot(lcv_ctx* ctx);
 static void be_stage_begin(lcv_ctx* ctx, int stage);
 static void be_stage_end(lcv_ctx* ctx, int stage);
 static void be_reset_timings(lcv_ctx* ctx);
@@ -71,7 +78,7 @@ static int hip_fail(lcv_ctx* ctx, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(ctx, _e, #x); \
   } while (0)
 
-static hipStream_t cur_stream(lcv_ctx* ctx) { return ctx->be.st[ctx->be.cur]; }
+static hipStream_t cur_stream(lcv_ctx* ctx) { return ctx->be.st[ctx->be.base + ctx->be.cur]; }
 
 static int be_init(lcv_ctx* ctx, int device) {
   int nd = 0;
@@ -84,6 +91,8 @@ static int be_init(lcv_ctx* ctx, int device) {
     HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.fork_ev[k], hipEventDisableTiming));
     HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.join_ev[k], hipEventDisableTiming));
   }
+  for (int s = 0; s < LCV_SLOTS; ++s)
+    for (int e = 0; e < EV_COUNT; ++e) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.ev[s][e], hipEventDisableTiming));
   return LCV_OK;
 }
 
@@ -95,6 +104,9 @@ static void be_destroy(lcv_ctx* ctx) {
     if (ctx->be.fork_ev[k]) (void)hipEventDestroy(ctx->be.fork_ev[k]);
     if (ctx->be.join_ev[k]) (void)hipEventDestroy(ctx->be.join_ev[k]);
   }
+  for (int s = 0; s < LCV_SLOTS; ++s)
+    for (int e = 0; e < EV_COUNT; ++e)
+      if (ctx->be.ev[s][e]) (void)hipEventDestroy(ctx->be.ev[s][e]);
 }
 
 static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
@@ -136,17 +148,36 @@ static int be_sync(lcv_ctx* ctx) {
   for (int k = BE_STREAMS - 1; k >= 0; --k) HIPCHK(ctx, hipStreamSynchronize(ctx->be.st[k]));
   return LCV_OK;
 }
-static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = (k > 0 && k < BE_STREAMS) ? k : 0; }
+static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = (k > 0 && ctx->be.base + k < BE_STREAMS) ? k : 0; }
+static void be_set_slot(lcv_ctx* ctx, int slot) {
+  ctx->be.base = 2 * slot;
+  ctx->be.cur = 0;
+}
+static int be_mark(lcv_ctx* ctx, int ev, int k) {
+  HIPCHK(ctx, hipEventRecord(ctx->be.ev[ctx->be.base / 2][ev], ctx->be.st[ctx->be.base + k]));
+  return LCV_OK;
+}
+static int be_wait(lcv_ctx* ctx, int k, int ev) {
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[ctx->be.base + k], ctx->be.ev[ctx->be.base / 2][ev], 0));
+  return LCV_OK;
+}
+static int be_sync_slot(lcv_ctx* ctx) {
+  HIPCHK(ctx, hipStreamSynchronize(ctx->be.st[ctx->be.base + 1]));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->be.st[ctx->be.base]));
+  return LCV_OK;
+}
 // stream k starts after everything queued so far on the main stream
 static int be_fork_to(lcv_ctx* ctx, int k) {
-  HIPCHK(ctx, hipEventRecord(ctx->be.fork_ev[k], ctx->be.st[0]));
-  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[k], ctx->be.fork_ev[k], 0));
+  const int b = ctx->be.base;
+  HIPCHK(ctx, hipEventRecord(ctx->be.fork_ev[b + k], ctx->be.st[b]));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[b + k], ctx->be.fork_ev[b + k], 0));
   return LCV_OK;
 }
 // the main stream continues after everything queued so far on stream k
 static int be_join_from(lcv_ctx* ctx, int k) {
-  HIPCHK(ctx, hipEventRecord(ctx->be.join_ev[k], ctx->be.st[k]));
-  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[0], ctx->be.join_ev[k], 0));
+  const int b = ctx->be.base;
+  HIPCHK(ctx, hipEventRecord(ctx->be.join_ev[b + k], ctx->be.st[b + k]));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->be.st[b], ctx->be.join_ev[b + k], 0));
   return LCV_OK;
 }
 static int be_fork(lcv_ctx* ctx) { return be_fork_to(ctx, 1); }
@@ -185,13 +216,13 @@ static hipEvent_t take_event(lcv_ctx* ctx) {
 static void be_stage_begin(lcv_ctx* ctx, int stage) {
   hipEvent_t e = take_event(ctx);
   if (!e) return;
-  const int k = ctx->be.cur;
+  const int k = ctx->be.base + ctx->be.cur;
   (void)hipEventRecord(e, cur_stream(ctx));
   ctx->be.open_stage[k] = stage;
   ctx->be.open_ev[k] = e;
 }
 static void be_stage_end(lcv_ctx* ctx, int stage) {
-  const int k = ctx->be.cur;
+  const int k = ctx->be.base + ctx->be.cur;
   if (ctx->be.open_stage[k] != stage || !ctx->be.open_ev[k]) return;
   hipEvent_t e = take_event(ctx);
   if (!e) return;
@@ -246,7 +277,7 @@ static void be_comm_destroy(lcv_ctx* ctx) {
 }
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank) {
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  ncclResult_t r = ncclAllGather(send, recv, per_rank, ncclUint8, ctx->be.comm, ctx->be.st[0]);
+  ncclResult_t r = ncclAllGather(send, recv, per_rank, ncclUint8, ctx->be.comm, cur_stream(ctx));
   return r == ncclSuccess ? LCV_OK : nccl_fail(ctx, r, "ncclAllGather");
 }
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {

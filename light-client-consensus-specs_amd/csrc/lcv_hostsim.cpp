@@ -54,6 +54,11 @@ static void be_use_stream(lcv_ctx* ctx, int k);
 static int be_fork_to(lcv_ctx*, int) { return 0; }
 static int be_join_from(lcv_ctx*, int) { return 0; }
 static int be_nstreams() { return 4; }
+// the host simulation runs every launch in program order: slots and events order nothing
+static void be_set_slot(lcv_ctx*, int) {}
+static int be_mark(lcv_ctx*, int, int) { return 0; }
+static int be_wait(lcv_ctx*, int, int) { return 0; }
+static int be_sync_slot(lcv_ctx*) { return 0; }
 static void be_stage_begin(lcv_ctx* ctx, int stage);
 static void be_stage_end(lcv_ctx* ctx, int stage);
 static void be_reset_timings(lcv_ctx* ctx);

@@ -190,6 +190,23 @@ class Verifier:
         self._check(self.lib.lcv_validate_resident_dev(self.ctx, rb.handle, int(current_slot), ptr(gvr),
                                                        C.c_void_p(verdict_dev_ptr)), "lcv_validate_resident_dev")
 
+    def validate_resident_async(self, rb: ResidentBatch, current_slot: int, genesis_validators_root: bytes,
+                                slot: int) -> None:
+        """Enqueue the whole pipeline for rb on work-space slot 0 or 1 and return at once (two batches
+        in flight); collect the verdicts with slot_wait(slot)."""
+        gvr = as_u8(bytes(genesis_validators_root))
+        self._keep_gvr = getattr(self, "_keep_gvr", {})
+        self._keep_gvr[slot] = gvr  # the call reads it before returning; kept for symmetry with the slot
+        self._check(self.lib.lcv_validate_resident_async(self.ctx, rb.handle, int(current_slot), ptr(gvr), int(slot)),
+                    "lcv_validate_resident_async")
+
+    def slot_wait(self, slot: int, n: int, verdict: Optional[np.ndarray] = None, reason: Optional[np.ndarray] = None):
+        """Wait for the batch of `slot`; its first n verdicts (bool) and reason codes."""
+        v = verdict if verdict is not None else np.zeros(n, np.uint8)
+        r = reason if reason is not None else np.zeros(n, np.uint8)
+        self._check(self.lib.lcv_slot_wait(self.ctx, int(slot), int(n), ptr(v), ptr(r)), "lcv_slot_wait")
+        return v, r
+
     # ------------------------------------------------------------------ BLS / SSZ primitives
     def fast_aggregate_verify(self, pubkeys: Sequence[bytes], message: bytes, signature: bytes) -> bool:
         pks = as_u8(b"".join(bytes(p) for p in pubkeys)) if len(pubkeys) else np.zeros(1, np.uint8)

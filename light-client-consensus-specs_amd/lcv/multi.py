@@ -83,6 +83,14 @@ class Comm:
                                                       int(per_rank), ptr(buf)), "lcv_validate_sharded")
         return buf
 
+    def slot_allgather(self, slot: int, n: int, per_rank: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """After this rank's batch in work-space slot `slot` (Verifier.validate_resident_async), all-gather
+        every rank's verdict bytes: (world * per_rank,) uint8, rank-major, each slice zero padded."""
+        buf = out if out is not None else np.zeros(self.world * per_rank, np.uint8)
+        self.v._check(self.v.lib.lcv_slot_allgather(self.v.ctx, int(slot), int(n), int(per_rank), ptr(buf)),
+                      "lcv_slot_allgather")
+        return buf
+
     def allreduce_max(self, x: float) -> float:
         d = C.c_double(float(x))
         self.v._check(self.v.lib.lcv_comm_allreduce_max(self.v.ctx, C.byref(d)), "lcv_comm_allreduce_max")

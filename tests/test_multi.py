@@ -1,6 +1,6 @@
 """N > 1 path on CPU: world_size-2 processes shard one batch, validate their shards on the host
 simulation of the kernels and all-gather the verdicts through lcv/multi.py's Comm — the same code and
-C ABI (lcv_comm_init, lcv_validate_sharded, lcv_comm_allreduce_max) bench.py runs over RCCL on the
+C ABI (lcv_comm_init, lcv_validate_sharded, lcv_slot_allgather, lcv_comm_allreduce_max) bench.py runs over RCCL on the
 GPUs; the host simulation's stand-in collective exchanges files.  A gloo run (torch.distributed) of
 the same shards checks the gathered verdicts independently."""
 import os
@@ -36,6 +36,14 @@ def _worker(rank, world, port, q):
         t = comm.allreduce_max(float(rank + 1))
         # independent check: gloo all-gather of the same shards' verdicts
         lo, hi = multi.shard_bounds(sb.updates.n, world, rank)
+        # two batches in flight (bench.py's serving loop): the shard in both work-space slots, the
+        # verdicts gathered per slot (lcv_slot_allgather)
+        rb = v.upload(sb.updates.slice(lo, hi))
+        per_rank = -(-sb.updates.n // world)
+        for s in (0, 1):
+            v.validate_resident_async(rb, sb.current_slot, sb.genesis_validators_root, s)
+        slots = [multi.unshard(comm.slot_allgather(s, hi - lo, per_rank), sb.updates.n, world).astype(bool).tolist()
+                 for s in (0, 1)]
         ok, _ = v.validate(sb.updates.slice(lo, hi), sb.current_slot, sb.genesis_validators_root)
         per = -(-sb.updates.n // world)
         buf = torch.zeros(per, dtype=torch.uint8)
@@ -44,7 +52,7 @@ def _worker(rank, world, port, q):
         dist.all_gather(parts, buf)
         gloo = multi.unshard(torch.cat(parts).numpy(), sb.updates.n, world).astype(bool)
         comm.close()
-        q.put((rank, full.tolist(), gloo.tolist(), sb.expected_verdict.tolist(), t))
+        q.put((rank, full.tolist(), gloo.tolist(), sb.expected_verdict.tolist(), t, slots))
     finally:
         dist.destroy_process_group()
 
@@ -72,6 +80,6 @@ def test_two_rank_gloo():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for rank, full, gloo, exp, t in res:
-        assert full == exp == gloo
+    for rank, full, gloo, exp, t, slots in res:
+        assert full == exp == gloo == slots[0] == slots[1]
         assert t == 2.0

@@ -28,3 +28,47 @@ def test_set_pipeline_rejects_bad_shapes():
         v.set_pipeline(0, 1)
     with pytest.raises(LcvError):
         v.set_pipeline(2, 0)
+
+
+def _two_batches(v, n=96):
+    from lcv import synth
+    kinds = synth.adversarial_kinds(n, seed=4, bad_fraction=0.25)
+    a = synth.generate(v, n, seed=4, participation="random", kinds=kinds)
+    b = synth.generate(v, n, seed=5, participation="random", kinds=synth.adversarial_kinds(n, seed=5, bad_fraction=0.25))
+    return a, b
+
+
+def check_async_slots(v):
+    """lcv_validate_resident_async / lcv_slot_wait: two batches in flight on slots 0 and 1, reused
+    twice each; every batch's verdicts and reasons equal the synchronous call's and its construction."""
+    a, b = _two_batches(v)
+    v.set_store(a.store_finalized_slot, a.current.ssz, a.next.ssz)
+    ra, rb = v.upload(a.updates), v.upload(b.updates)
+    sync_a = v.validate_resident(ra, a.current_slot, a.genesis_validators_root)
+    assert np.array_equal(sync_a[1], a.expected_reason)
+    for rep in range(2):
+        v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 0)
+        v.validate_resident_async(rb, b.current_slot, b.genesis_validators_root, 1)
+        va, za = v.slot_wait(0, len(a.expected_reason))
+        vb, zb = v.slot_wait(1, len(b.expected_reason))
+        assert np.array_equal(za, a.expected_reason) and np.array_equal(va, sync_a[0])
+        assert np.array_equal(zb, b.expected_reason) and np.array_equal(vb.astype(bool), zb == 0)
+    # a synchronous call after async ones still uses slot 0 and agrees
+    again = v.validate_resident(ra, a.current_slot, a.genesis_validators_root)
+    assert np.array_equal(again[1], sync_a[1])
+
+
+def test_async_slots_hostsim():
+    check_async_slots(H.hostsim_verifier())
+
+
+def test_async_rejects_bad_slot():
+    from lcv._native import LcvError
+    v = H.hostsim_verifier()
+    a, _ = _two_batches(v, 8)
+    v.set_store(a.store_finalized_slot, a.current.ssz, a.next.ssz)
+    ra = v.upload(a.updates)
+    with pytest.raises(LcvError):
+        v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 2)
+    with pytest.raises(LcvError):
+        v.slot_wait(1, 10 ** 6)
