@@ -9,14 +9,14 @@ aggregation, Miller loop, final exponentiation, verdicts).  Inputs are resident 
 once, outside the timed region); for N > 1 each step ends with an RCCL all-gather of the per-rank
 verdict bytes (the only collective of the design).  Weak scaling: every rank owns `--n` updates.
 
-Default shape (--depth 2): the serving loop keeps two batches in flight — two resident batches of
-`--n` updates alternate over the two work-space slots of the context (lcv_validate_resident_async), so
-batch k+1's latency-bound early stages (SSWU, hash_to_G2) share the GPU with batch k's Miller loop and
-final exponentiation; each timed step is one whole batch, waited for and its verdicts read (or
+Default shape (--depth 4): the serving loop keeps four batches in flight — four resident batches of
+`--n` updates rotate over the work-space slots of the context (lcv_validate_resident_async), so later
+batches' latency-bound early stages (SSWU, hash_to_G2) share the GPU with earlier batches' Miller loop
+and final exponentiation; each timed step is one whole batch, waited for and its verdicts read (or
 all-gathered) inside the timed region.  --depth 1 times one batch at a time; both rates are reported.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n UPDATES_PER_GPU] [--participation full|random]
-                    [--depth 1|2]
+                    [--depth 1..4]
 """
 from __future__ import annotations
 
@@ -30,6 +30,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "light-client-consensus-specs_amd"))
 
 import numpy as np  # noqa: E402
+
+DEFAULT_DEPTH = 4
+# one HIP stream pair per work-space slot: with HIP's default of 4 hardware queues per process the 8
+# streams of 4 slots would share queues (ordering more than the events require); gpurun allows <= 32
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 PEAK_INT32_TOPS = 39.3  # 256 CU x 64 lanes x 2.4 GHz; the box-measured mad rate is reported beside it
 
@@ -96,8 +102,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[2]/[3]/[4] lines")
     ap.add_argument("--pipeline", default="1,1", help="STREAMS,SLICES of the timed run (1,1 = serial stages)")
-    ap.add_argument("--depth", type=int, default=2, choices=[1, 2],
-                    help="batches in flight: 2 = double-buffered serving loop over two work-space slots "
+    ap.add_argument("--depth", type=int, default=DEFAULT_DEPTH, choices=[1, 2, 3, 4],
+                    help="batches in flight: D > 1 = serving loop over D work-space slots "
                          "(lcv_validate_resident_async), 1 = one batch at a time")
     args = ap.parse_args()
 
@@ -116,11 +122,11 @@ def main():
     log(f"[rank {rank}] generated {args.n} updates in {time.perf_counter() - t0:.1f}s")
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     rb = v.upload(sb.updates)
-    # depth 2: a second, different batch of the same shape (same store), so the two slots alternate
-    # between two resident batches
-    sb2 = synth.generate(v, args.n, seed=1002 + rank, participation=args.participation) if args.depth == 2 else sb
-    rbs = [rb, v.upload(sb2.updates) if args.depth == 2 else rb]
-    sbs = [sb, sb2]
+    # depth D > 1: D different resident batches of the same shape (same store), one per work-space slot
+    D = args.depth
+    sbs = [sb] + [synth.generate(v, args.n, seed=1000 * k + 2 + rank, participation=args.participation)
+                  for k in range(1, D)]
+    rbs = [rb] + [v.upload(b.updates) for b in sbs[1:]]
     pipe = tuple(int(x) for x in args.pipeline.split(","))
     v.set_pipeline(*pipe)
     verdict = np.zeros(args.n, np.uint8)
@@ -138,10 +144,10 @@ def main():
         if comm is not None:
             comm.barrier()
 
-    slot_ok = [True, True]
-    per_slot_v = [np.zeros(args.n, np.uint8), np.zeros(args.n, np.uint8)]
-    per_slot_r = [np.zeros(args.n, np.uint8), np.zeros(args.n, np.uint8)]
-    per_slot_g = [np.zeros(world * args.n, np.uint8), np.zeros(world * args.n, np.uint8)]
+    slot_ok = [True] * D
+    per_slot_v = [np.zeros(args.n, np.uint8) for _ in range(D)]
+    per_slot_r = [np.zeros(args.n, np.uint8) for _ in range(D)]
+    per_slot_g = [np.zeros(world * args.n, np.uint8) for _ in range(D)]
 
     def collect(s):  # wait for slot s's batch; its verdicts (all-gathered over RCCL when N > 1)
         if comm is None:
@@ -152,20 +158,20 @@ def main():
             slot_ok[s] = slot_ok[s] and bool((per_slot_g[s] == 1).all())
 
     def stream_steps(k_steps):
-        # double-buffered serving loop: batch k runs in slot k % 2 while batch k - 1 is still on the GPU;
-        # the host waits for a slot (and reads its verdicts) only before reusing it, and drains both
+        # serving loop: batch k runs in slot k % D while batches k - D + 1 .. k - 1 are still on the GPU;
+        # the host waits for a slot (and reads its verdicts) only before reusing it, and drains them all
         for k in range(k_steps):
-            s = k % 2
-            if k >= 2:
+            s = k % D
+            if k >= D:
                 collect(s)
             v.validate_resident_async(rbs[s], sbs[s].current_slot, sbs[s].genesis_validators_root, s)
-        for k in range(max(0, k_steps - 2), k_steps):
-            collect(k % 2)
+        for k in range(max(0, k_steps - D), k_steps):
+            collect(k % D)
 
     for _ in range(args.warmup):
         step()
-    if args.depth == 2:
-        stream_steps(max(2, args.warmup))
+    if D > 1:
+        stream_steps(max(D, args.warmup))
     # correctness of what is timed: every synthetic update is valid
     if comm is None:
         v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root, verdict, reason)
@@ -177,7 +183,7 @@ def main():
     stage_ms = {k: 0.0 for k in v.last_timings()}
     sync()
     t0 = time.perf_counter()
-    if args.depth == 2:
+    if D > 1:
         stream_steps(args.steps)
     else:
         for _ in range(args.steps):
@@ -189,7 +195,7 @@ def main():
     dt = time.perf_counter() - t0
     if comm is not None:
         dt = comm.allreduce_max(dt)
-    if args.depth == 2:
+    if D > 1:
         ok_all = ok_all and all(slot_ok)
 
     serial_ms, serial_ok = 1000 * dt / args.steps, ok_all
@@ -260,10 +266,10 @@ def main():
         "stage_kernel_ms_per_step": stage_avg,
         "sum_of_stage_kernel_ms": round(kernel_ms, 3),
         "value_is": ("kernel-only: inputs resident in HBM (uploaded once); " +
-                     ("two batches in flight (double-buffered serving loop over two work-space slots, "
-                      "lcv_validate_resident_async): batch k+1's stages overlap batch k's, every batch's "
+                     (f"{D} batches in flight (serving loop over {D} work-space slots, "
+                      "lcv_validate_resident_async): later batches' stages overlap earlier ones', every batch's "
                       "verdicts are waited for and copied out (all-gathered over RCCL for N > 1) inside the "
-                      "timed region; " if args.depth == 2 else "") +
+                      "timed region; " if D > 1 else "") +
                      "pcie_inclusive_* copies the packed batch host->device and the verdicts back in every call"),
         "pcie_inclusive_updates_per_s_1gpu": round(pcie_rate, 1),
         "roofline": roof,

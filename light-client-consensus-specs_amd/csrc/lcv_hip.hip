@@ -16,7 +16,9 @@
 
 struct lcv_ctx;
 
-enum { BE_STREAMS = 4 };  // GPU_MAX_HW_QUEUES on the box: one hardware queue per stream
+// two streams per work-space slot; a stream per hardware queue when GPU_MAX_HW_QUEUES >= 8 (bench.py sets
+// it; with HIP's default of 4 the streams share queues, which orders more than the events require)
+enum { BE_STREAMS = 2 * LCV_SLOTS };
 struct Backend {
   hipStream_t st[BE_STREAMS] = {};  // st[0]: main stream (copies, serial stages); st[k]: forked work
   int cur = 0;                      // stream of the next launch / copy
@@ -25,7 +27,7 @@ struct Backend {
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   std::vector<Mark> marks;
-  int open_stage[BE_STREAMS] = {-1, -1, -1, -1};
+  int open_stage[BE_STREAMS] = {-1, -1, -1, -1, -1, -1, -1, -1};
   hipEvent_t open_ev[BE_STREAMS] = {};
   hipEvent_t fork_ev[BE_STREAMS] = {}, join_ev[BE_STREAMS] = {};
   int base = 0;                          // work-space slot s uses streams st[2s] (main), st[2s + 1] (side)

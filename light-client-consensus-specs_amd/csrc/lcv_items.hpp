@@ -247,7 +247,7 @@ LCV_FN void item_pre(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
 }
 
 // :460-463 fork version, domain and signing root of the attested header -> W.msg.  A kernel of its own
-// (~10 SHA-256 compressions per update against item_pre's ~170), so hash_to_G2 starts without waiting
+// (16 SHA-256 compressions per update against item_pre's 162), so hash_to_G2 starts without waiting
 // for the branch checks, which run beside it on another stream.
 LCV_FN void item_sigroot(uint32_t i, const BatchDev& B, const Params& P, const Work& W) {
   const uint8_t* ab = B.att_beacon + (size_t)K_BEACON * i;

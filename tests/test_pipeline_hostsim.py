@@ -53,6 +53,13 @@ def check_async_slots(v):
         vb, zb = v.slot_wait(1, len(b.expected_reason))
         assert np.array_equal(za, a.expected_reason) and np.array_equal(va, sync_a[0])
         assert np.array_equal(zb, b.expected_reason) and np.array_equal(vb.astype(bool), zb == 0)
+    # four batches in flight: every slot of the context, a and b alternating
+    for s in range(4):
+        x = (a, ra) if s % 2 == 0 else (b, rb)
+        v.validate_resident_async(x[1], x[0].current_slot, x[0].genesis_validators_root, s)
+    for s in range(4):
+        exp = a.expected_reason if s % 2 == 0 else b.expected_reason
+        assert np.array_equal(v.slot_wait(s, len(exp))[1], exp)
     # a synchronous call after async ones still uses slot 0 and agrees
     again = v.validate_resident(ra, a.current_slot, a.genesis_validators_root)
     assert np.array_equal(again[1], sync_a[1])
@@ -69,6 +76,6 @@ def test_async_rejects_bad_slot():
     v.set_store(a.store_finalized_slot, a.current.ssz, a.next.ssz)
     ra = v.upload(a.updates)
     with pytest.raises(LcvError):
-        v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 2)
+        v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 4)
     with pytest.raises(LcvError):
         v.slot_wait(1, 10 ** 6)

@@ -12,5 +12,5 @@ timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 echo "smoke ok" &&
 timeout -k 10 400 python -u bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err &&
 echo "bench ok" &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-configs > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --depth 1 --steps 3 --warmup 1 --no-cpu-baseline --no-configs > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err &&
 echo "rocprof ok"
