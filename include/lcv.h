@@ -206,6 +206,8 @@ int lcv_sign_batch(lcv_ctx* ctx, const uint8_t* sk32, const uint8_t* msg32, uint
 
 /* ---- parity-test entry points (intermediate values, canonical big-endian bytes) */
 /* field ops on (a, b) < p: out per item = a*b, a+b, a-b, a^-1, sqrt_fp2(a + b u) (2 x 48); ok = sqrt exists */
+/* test hook: rows per validate chunk (multiple of 64, <= 65536; default 65536) */
+int lcv_debug_set_chunk(lcv_ctx* ctx, uint64_t rows);
 int lcv_debug_fp(lcv_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint64_t n, uint8_t* out288, uint8_t* ok);
 /* a^((p+1)/4) || a^((p-3)/4) (2 x 48 B) for a < p: the windowed sqrt exponentiations of decompression / SSWU */
 int lcv_debug_fp_pow(lcv_ctx* ctx, const uint8_t* a48, uint64_t n, uint8_t* out96);

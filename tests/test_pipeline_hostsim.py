@@ -79,3 +79,27 @@ def test_async_rejects_bad_slot():
         v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 4)
     with pytest.raises(LcvError):
         v.slot_wait(1, 10 ** 6)
+
+
+def test_chunks_rotate_over_slots_hostsim():
+    """A batch of several chunks (64-row chunks here, 65,536 in production): chunks rotate over the four
+    work-space slots, each slot's first chunk hashing the committee pool; every verdict and reason equals
+    the one-chunk call's and the construction (ragged last chunk, more chunks than slots)."""
+    import ctypes as C
+    from lcv import synth
+    v = H.hostsim_verifier()
+    n = 64 * 6 + 17
+    kinds = synth.adversarial_kinds(n, seed=12, bad_fraction=0.2)
+    sb = synth.generate(v, n, seed=12, participation="random", kinds=kinds, npool=3)
+    v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    ok1, r1 = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    assert np.array_equal(r1, sb.expected_reason)
+    v._check(v.lib.lcv_debug_set_chunk(v.ctx, C.c_uint64(64)), "lcv_debug_set_chunk")
+    try:
+        ok2, r2 = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+        rb = v.upload(sb.updates)
+        ok3, r3 = v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root)
+    finally:
+        v._check(v.lib.lcv_debug_set_chunk(v.ctx, C.c_uint64(65536)), "lcv_debug_set_chunk")
+    assert np.array_equal(r2, r1) and np.array_equal(ok2, ok1)
+    assert np.array_equal(r3, r1) and np.array_equal(ok3.astype(bool), ok1)
