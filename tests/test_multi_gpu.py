@@ -1,6 +1,6 @@
 """The RCCL path of lcv/multi.py on the GPU with one rank (the box has one GPU; the driver's 8-GPU
 scaling run exercises more ranks): communicator init from a rendezvous id, sharded validate with the
-device-to-device verdict all-gather, the max all-reduce used for bench timing, and teardown."""
+device-to-device verdict all-gather (also per work-space slot, lcv_slot_allgather), the max all-reduce used for bench timing, and teardown."""
 import os
 
 import numpy as np
@@ -26,6 +26,16 @@ def test_rccl_one_rank(gpu_verifier):
         finally:
             rb.free()
         assert list(g[:len(kinds)].astype(bool)) == list(sb.expected_verdict) and not g[len(kinds):].any()
+        # bench.py's N > 1 serving loop: batches in flight on every slot, verdicts all-gathered per slot
+        rb = gpu_verifier.upload(sb.updates)
+        try:
+            for s in range(4):
+                gpu_verifier.validate_resident_async(rb, sb.current_slot, sb.genesis_validators_root, s)
+            for s in range(4):
+                g = comm.slot_allgather(s, len(kinds), 16)
+                assert list(g[:len(kinds)].astype(bool)) == list(sb.expected_verdict) and not g[len(kinds):].any()
+        finally:
+            rb.free()
         assert comm.allreduce_max(3.5) == 3.5
     finally:
         comm.close()
