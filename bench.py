@@ -32,10 +32,10 @@ sys.path.insert(0, os.path.join(ROOT, "light-client-consensus-specs_amd"))
 import numpy as np  # noqa: E402
 
 DEFAULT_DEPTH = 4
-# one HIP stream pair per work-space slot: with HIP's default of 4 hardware queues per process the 8
-# streams of 4 slots would share queues (ordering more than the events require); gpurun allows <= 32
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# one HIP stream pair per work-space slot: with HIP's default of 4 hardware queues per process the
+# streams of several slots would share queues (ordering more than the events require); gpurun allows <= 32
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 PEAK_INT32_TOPS = 39.3  # 256 CU x 64 lanes x 2.4 GHz; the box-measured mad rate is reported beside it
 
@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[2]/[3]/[4] lines")
     ap.add_argument("--pipeline", default="1,1", help="STREAMS,SLICES of the timed run (1,1 = serial stages)")
-    ap.add_argument("--depth", type=int, default=DEFAULT_DEPTH, choices=[1, 2, 3, 4],
+    ap.add_argument("--depth", type=int, default=DEFAULT_DEPTH, choices=range(1, 9),
                     help="batches in flight: D > 1 = serving loop over D work-space slots "
                          "(lcv_validate_resident_async), 1 = one batch at a time")
     args = ap.parse_args()

@@ -122,7 +122,7 @@ int lcv_validate_resident_dev(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot
                               const uint8_t* genesis_validators_root, uint8_t* verdict_dev);
 /* Several batches in flight (multi-buffered serving loop; no reference counterpart: the reference
  * validates one update per call, sync-protocol.md:386).  lcv_validate_resident_async enqueues the whole
- * pipeline for b (at most 65536 updates) on the two HIP streams of work-space slot `slot` (0..3) and
+ * pipeline for b (at most 65536 updates) on the two HIP streams of work-space slot `slot` (0..7) and
  * returns without waiting; lcv_slot_wait waits for that slot and copies the first n verdicts / reason
  * codes out (either pointer may be NULL).  A slot's next batch starts on the device after its previous
  * one; alternate the slots and wait for a slot before reading or reusing it. */

@@ -2,8 +2,8 @@
 // and the host-simulation test build (liblcv_hostsim.so, g++: the same per-item code run on
 // CPU so that the arithmetic can be checked against the oracle without a GPU).
 #pragma once
-// work-space slots of a context (up to four batches in flight) and the events that order a slot's two streams
-enum { LCV_SLOTS = 4 };
+// work-space slots of a context (up to eight batches in flight) and the events that order a slot's two streams
+enum { LCV_SLOTS = 8 };
 enum { EV_START = 0, EV_PRE, EV_H2C, EV_SIDE, EV_COUNT };
 #include <stddef.h>
 #include <stdint.h>

@@ -16,8 +16,9 @@
 
 struct lcv_ctx;
 
-// two streams per work-space slot; a stream per hardware queue when GPU_MAX_HW_QUEUES >= 8 (bench.py sets
-// it; with HIP's default of 4 the streams share queues, which orders more than the events require)
+// two streams per work-space slot; a stream per hardware queue when GPU_MAX_HW_QUEUES >= 2 x the slots in
+// use (bench.py sets it; with HIP's default of 4 the streams share queues, which orders more than the
+// events require)
 enum { BE_STREAMS = 2 * LCV_SLOTS };
 struct Backend {
   hipStream_t st[BE_STREAMS] = {};  // st[0]: main stream (copies, serial stages); st[k]: forked work
@@ -27,7 +28,7 @@ struct Backend {
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   std::vector<Mark> marks;
-  int open_stage[BE_STREAMS] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  int open_stage[BE_STREAMS];  // set to -1 by be_init
   hipEvent_t open_ev[BE_STREAMS] = {};
   hipEvent_t fork_ev[BE_STREAMS] = {}, join_ev[BE_STREAMS] = {};
   int base = 0;                          // work-space slot s uses streams st[2s] (main), st[2s + 1] (side)
@@ -95,6 +96,7 @@ static int be_init(lcv_ctx* ctx, int device) {
   }
   for (int s = 0; s < LCV_SLOTS; ++s)
     for (int e = 0; e < EV_COUNT; ++e) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->be.ev[s][e], hipEventDisableTiming));
+  for (int k = 0; k < BE_STREAMS; ++k) ctx->be.open_stage[k] = -1;
   return LCV_OK;
 }
 

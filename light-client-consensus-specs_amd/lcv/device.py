@@ -192,7 +192,7 @@ class Verifier:
 
     def validate_resident_async(self, rb: ResidentBatch, current_slot: int, genesis_validators_root: bytes,
                                 slot: int) -> None:
-        """Enqueue the whole pipeline for rb on work-space slot 0..3 and return at once (up to four
+        """Enqueue the whole pipeline for rb on work-space slot 0..7 and return at once (up to eight
         batches in flight); collect the verdicts with slot_wait(slot)."""
         gvr = as_u8(bytes(genesis_validators_root))
         self._keep_gvr = getattr(self, "_keep_gvr", {})

@@ -29,9 +29,9 @@ def test_rccl_one_rank(gpu_verifier):
         # bench.py's N > 1 serving loop: batches in flight on every slot, verdicts all-gathered per slot
         rb = gpu_verifier.upload(sb.updates)
         try:
-            for s in range(4):
+            for s in range(8):
                 gpu_verifier.validate_resident_async(rb, sb.current_slot, sb.genesis_validators_root, s)
-            for s in range(4):
+            for s in range(8):
                 g = comm.slot_allgather(s, len(kinds), 16)
                 assert list(g[:len(kinds)].astype(bool)) == list(sb.expected_verdict) and not g[len(kinds):].any()
         finally:

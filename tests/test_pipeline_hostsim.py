@@ -53,11 +53,11 @@ def check_async_slots(v):
         vb, zb = v.slot_wait(1, len(b.expected_reason))
         assert np.array_equal(za, a.expected_reason) and np.array_equal(va, sync_a[0])
         assert np.array_equal(zb, b.expected_reason) and np.array_equal(vb.astype(bool), zb == 0)
-    # four batches in flight: every slot of the context, a and b alternating
-    for s in range(4):
+    # eight batches in flight: every slot of the context, a and b alternating
+    for s in range(8):
         x = (a, ra) if s % 2 == 0 else (b, rb)
         v.validate_resident_async(x[1], x[0].current_slot, x[0].genesis_validators_root, s)
-    for s in range(4):
+    for s in range(8):
         exp = a.expected_reason if s % 2 == 0 else b.expected_reason
         assert np.array_equal(v.slot_wait(s, len(exp))[1], exp)
     # a synchronous call after async ones still uses slot 0 and agrees
@@ -76,19 +76,19 @@ def test_async_rejects_bad_slot():
     v.set_store(a.store_finalized_slot, a.current.ssz, a.next.ssz)
     ra = v.upload(a.updates)
     with pytest.raises(LcvError):
-        v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 4)
+        v.validate_resident_async(ra, a.current_slot, a.genesis_validators_root, 8)
     with pytest.raises(LcvError):
         v.slot_wait(1, 10 ** 6)
 
 
 def test_chunks_rotate_over_slots_hostsim():
-    """A batch of several chunks (64-row chunks here, 65,536 in production): chunks rotate over the four
+    """A batch of several chunks (64-row chunks here, 65,536 in production): chunks rotate over the eight
     work-space slots, each slot's first chunk hashing the committee pool; every verdict and reason equals
     the one-chunk call's and the construction (ragged last chunk, more chunks than slots)."""
     import ctypes as C
     from lcv import synth
     v = H.hostsim_verifier()
-    n = 64 * 6 + 17
+    n = 64 * 10 + 17
     kinds = synth.adversarial_kinds(n, seed=12, bad_fraction=0.2)
     sb = synth.generate(v, n, seed=12, participation="random", kinds=kinds, npool=3)
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
