@@ -430,8 +430,31 @@ def config_lines(v) -> dict:
                 "valid_fraction": round(float((sb.expected_reason == 0).mean()), 4), "stage_kernel_ms": stages}
     t0 = time.perf_counter()
     base = synth.generate(v, 15625, seed=3, participation="random")
-    out["configs[2]"] = timed(synth.tile(base, 8), "125,000 updates (the 1M / 8-GPU batch's per-GPU shard), "
-                                                   "random participation 342..512")
+    sb2 = synth.tile(base, 8)
+    out["configs[2]"] = timed(sb2, "125,000 updates (the 1M / 8-GPU batch's per-GPU shard), "
+                                   "random participation 342..512")
+    # the masked pubkey gather of g1_aggregate (north star: HBM GB/s of the gather): a lane reads the
+    # affine points (96 B) of the non-participants (> 256 participants: subtracted from the committee's
+    # precomputed sum) or of the participants (<= 256) from the resident 49 KB committee table
+    # measured on one 15,625-row chunk validated alone (the multi-chunk passes above overlap their
+    # chunks on the work-space slots, so their per-stage event times include other chunks' kernels)
+    pc = np.unpackbits(base.updates.sync_bits, axis=1).sum(axis=1)
+    gathered = np.where(pc > 256, 512 - pc, pc).astype(np.float64) * 96
+    v.set_store(base.store_finalized_slot, base.current.ssz, base.next.ssz)
+    rb = v.upload(base.updates)
+    try:
+        for _ in range(2):
+            v.validate_resident(rb, base.current_slot, base.genesis_validators_root)
+        agg_ms = v.last_timings().get("g1_aggregate", 0.0)
+    finally:
+        rb.free()
+    out["configs[2]"]["pubkey_gather"] = {
+        "rows": base.updates.n, "bytes_per_update": round(float(gathered.mean()), 1),
+        "g1_aggregate_ms": round(agg_ms, 3),
+        "GB_per_s": round(float(gathered.sum()) / (agg_ms * 1e-3) / 1e9, 1) if agg_ms else None,
+        "note": "algorithmic bytes / g1_aggregate kernel time (k_team<F_agg_team>, 4 lanes per update); the "
+                "2 x 512-point table stays in L2/MALL, so this is gather bandwidth from cache, far below "
+                "the 8 TB/s HBM roofline (each lane runs a chain of mixed additions)"}
     sb3 = synth.generate(v, 10000, seed=4, npool=10000)
     out["configs[3]"] = timed(sb3, "10,000 Deneb updates, all branches, a DISTINCT next_sync_committee each "
                                    "(HTR(SyncCommittee) per update)")

@@ -20,6 +20,14 @@ struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32
 struct F_agg_fold { Work W; uint32_t m; LCV_HD void operator()(uint32_t) const { item_agg_fold(m, W); } };
 struct F_verdict { Work W; LCV_HD void operator()(uint32_t i) const { item_verdict(i, W); } };
 struct F_key { CommitteeDev C; LCV_HD void operator()(uint32_t t) const { item_committee_key(t, C); } };
+struct F_agg_team {  // AGG_TEAM lanes per update (item_agg_team)
+  BatchDev B; CommitteeDev C; Work W;
+  static constexpr uint32_t TEAM = AGG_TEAM, LDS_WORDS = AGG_LDS, SHARED_WORDS = 0;
+  LCV_HD uint32_t rounds() const { return AGG_ROUNDS; }
+  LCV_HD void operator()(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, uint32_t*) const {
+    item_agg_team(i, lane, r, lds, B, C, W);
+  }
+};
 struct F_sum {  // one wave per committee (item_committee_sum_team)
   CommitteeDev C;
   static constexpr uint32_t TEAM = SUM_TEAM, LDS_WORDS = SUM_LDS, SHARED_WORDS = 0;

@@ -337,6 +337,81 @@ LCV_FN void item_agg(uint32_t i, const BatchDev& B, const CommitteeDev& C, const
   W.agg_status[i] = (uint8_t)(anybad ? PT_BAD : (inf || pc == 0 ? PT_INF : PT_OK));
 }
 
+// Jacobian G1 point <-> 36 LDS words (team kernels)
+LCV_FN void ld_g1j_lds(g1j& p, const uint32_t* s) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { p.x.v[k] = s[k]; p.y.v[k] = s[12 + k]; p.z.v[k] = s[24 + k]; }
+}
+LCV_FN void st_g1j_lds(uint32_t* s, const g1j& p) {
+  LCV_UNROLL for (int k = 0; k < 12; ++k) { s[k] = p.x.v[k]; s[12 + k] = p.y.v[k]; s[24 + k] = p.z.v[k]; }
+}
+
+// The same masked aggregation on a team of AGG_TEAM = 4 lanes per item (16 items per wave): round 0,
+// lane l sums the gathered points of mask words 4l .. 4l + 3 (128 keys); rounds 1-2, a pairwise tree
+// over the 4 partial sums in LDS; round 3, lane 0 adds the committee sum (complement case), converts to
+// affine and writes the aggregate.  One lane per item ran a serial chain as long as the wave's longest
+// (up to 170 mixed additions at 342-512 random participants); here each lane's chain covers a quarter
+// of the bits (north star: wavefront-level reductions for point aggregation).
+enum { AGG_TEAM = 4, AGG_ROUNDS = 4, AGG_LDS = AGG_TEAM * 36 };
+LCV_FN void item_agg_team(uint32_t i, uint32_t lane, uint32_t r, uint32_t* lds, const BatchDev& B,
+                          const CommitteeDev& C, const Work& W) {
+  const uint32_t c = W.comm_id[i];
+  const uint32_t* bw = (const uint32_t*)(B.bits + 64 * (size_t)i);
+  const uint32_t* bad = C.badmask + 16 * c;
+  uint32_t* part = lds + 36 * lane;
+  if (r == 0) {
+    uint32_t pc = 0;
+    LCV_UNROLL for (int w = 0; w < 16; ++w) pc += (uint32_t)__builtin_popcount(bw[w]);
+    const bool comp = pc > 256;
+    const uint32_t* pts = C.pts + (size_t)c * 512 * 24;
+    g1j acc;
+    jac_set_inf(acc);
+    LCV_NOUNROLL for (uint32_t w = 4 * lane; w < 4 * lane + 4; ++w) {
+      uint32_t m = comp ? (~bw[w] & ~bad[w]) : bw[w];
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        g1a p;
+        ld_g1a_tbl(p, pts, 32 * w + b);
+        if (comp) fp_neg(p.y, p.y);
+        jac_madd(acc, acc, p);
+      }
+    }
+    st_g1j_lds(part, acc);
+  } else if (r < AGG_ROUNDS - 1) {
+    const uint32_t step = 1u << (r - 1);
+    if ((lane & (2 * step - 1)) == 0) {
+      g1j a, b;
+      ld_g1j_lds(b, lds + 36 * (lane + step));
+      if (!jac_is_inf(b)) {
+        ld_g1j_lds(a, part);
+        jac_add(a, a, b);
+        st_g1j_lds(part, a);
+      }
+    }
+  } else if (lane == 0) {
+    uint32_t pc = 0, anybad = 0;
+    LCV_UNROLL for (int w = 0; w < 16; ++w) {
+      pc += (uint32_t)__builtin_popcount(bw[w]);
+      anybad |= bw[w] & bad[w];
+    }
+    g1j acc;
+    ld_g1j_lds(acc, part);
+    if (pc > 256) {  // sum_all - sum(non-participants)
+      g1j all;
+      const uint32_t* s = C.sum_all + 36 * c;
+      LCV_UNROLL for (int k = 0; k < 12; ++k) { all.x.v[k] = s[k]; all.y.v[k] = s[12 + k]; all.z.v[k] = s[24 + k]; }
+      if (jac_is_inf(acc)) acc = all;
+      else jac_add(acc, acc, all);
+    }
+    const bool inf = jac_is_inf(acc);
+    g1a a;
+    jac_to_aff(a, acc);
+    soa_st_fp(W.pk, W.cap, i, 0, a.x);
+    soa_st_fp(W.pk, W.cap, i, 1, a.y);
+    W.agg_status[i] = (uint8_t)(anybad ? PT_BAD : (inf || pc == 0 ? PT_INF : PT_OK));
+  }
+}
+
 // FastAggregateVerify with more keys than one 512-key table: items 0..m-1 hold the masked aggregates
 // of consecutive 512-key slices of the caller's list; item 0 becomes their sum (any invalid key ->
 // PT_BAD, an identity sum -> PT_INF).  One lane; m = ceil(npk / 512) is small.
@@ -389,12 +464,6 @@ LCV_FN void item_committee_key(uint32_t t, const CommitteeDev& C) {
 // validity byte; rounds 1..6, a pairwise tree over the 64 partial sums in LDS (lane l adds lane
 // l + 2^(k-1)'s sum when l % 2^k == 0); round 7 writes the sum and the 16 mask words.
 enum { SUM_TEAM = 64, SUM_ROUNDS = 8, SUM_LDS = 64 * 36 + 16 };
-LCV_FN void ld_g1j_lds(g1j& p, const uint32_t* s) {
-  LCV_UNROLL for (int k = 0; k < 12; ++k) { p.x.v[k] = s[k]; p.y.v[k] = s[12 + k]; p.z.v[k] = s[24 + k]; }
-}
-LCV_FN void st_g1j_lds(uint32_t* s, const g1j& p) {
-  LCV_UNROLL for (int k = 0; k < 12; ++k) { s[k] = p.x.v[k]; s[12 + k] = p.y.v[k]; s[24 + k] = p.z.v[k]; }
-}
 LCV_FN void item_committee_sum_team(uint32_t c, uint32_t lane, uint32_t r, uint32_t* lds, const CommitteeDev& C) {
   uint32_t* part = lds + 36 * lane;
   uint8_t* mbytes = (uint8_t*)(lds + 64 * 36);
