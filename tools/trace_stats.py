@@ -24,6 +24,8 @@ def grid_for(name: str, n: int):
     if kind == "k_sop":
         team = SOP_TEAM.get(f)
         return {-(-n // (64 // team)) * 64} if team else None
+    if kind == "k_team" and f == "F_agg_team":  # 4 lanes per update, 16 updates per wave
+        return {-(-n // 16) * 64}
     if kind == "k_items":
         items = 2 * n if f == "F_h2c_map" else n
         return {-(-items // 64) * 64}
