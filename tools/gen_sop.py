@@ -592,17 +592,19 @@ def line_program(team=10):
                 [Op(dst_of(J[c]), fp2_sqr(X, c)) for c in range(2)] +
                 [Op(dst_of(XY[c]), fp2_prod(X, Y, c)) for c in range(2)] +
                 [Op(dst_of(YZ[c]), fp2_prod(Y, Z, c)) for c in range(2)])
-        # line: a = B - 12 C', b = 3 J * nxP, c = 2 YZ * yP ;  B -+ 3E with E = 12 C'
+        # line: a = B - 12 C', b = 3 J * nxP, c = 2 YZ * yP ;  B -+ 3E with E = 12 C'.  This round holds
+        # only the add-in combinations (no products: one REDC of cost); b and c, single products of
+        # round-one values, ride in the next round's idle lanes (it has 6 ops of K = 2 on 10 lanes)
         ops = [Op(dst_of(BmF[c]), [], [(B[c].slot, 1), (Cp[c].slot, -36)]) for c in range(2)]
         ops += [Op(dst_of(BpF[c]), [], [(B[c].slot, 1), (Cp[c].slot, 36)]) for c in range(2)]
         ops += [Op(dst_of(la[c]), [], [(B[c].slot, 1), (Cp[c].slot, -12)], emit=6 * step + c) for c in range(2)]
-        ops += [Op(dst_of(lb[c]), [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
-        ops += [Op(dst_of(lc[c]), [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
         p.round(ops)
         # T: X = 2 XY (B - 3E), Y = (B + 3E)^2 - 1728 C'^2, Z = 8 B YZ
         ops = [Op(dst_of(X[c]), fp2_prod(XY, BmF, c, m=2)) for c in range(2)]
         ops += [Op(dst_of(Y[c]), fp2_sqr(BpF, c) + fp2_sqr(Cp, c, m=-1728)) for c in range(2)]
         ops += [Op(dst_of(Z[c]), fp2_prod(B, YZ, c, m=8)) for c in range(2)]
+        ops += [Op(dst_of(lb[c]), [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
+        ops += [Op(dst_of(lc[c]), [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
         p.round(ops)
         step += 1
         if bit == "1":
