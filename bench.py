@@ -94,8 +94,8 @@ def cpu_baseline(target_s: float = 15.0, seed: int = 3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--n", type=int, default=10000, help="updates per GPU (configs[1]: 10,000)")
     ap.add_argument("--participation", default="full", choices=["full", "random"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample size in seconds")
