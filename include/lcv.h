@@ -125,7 +125,8 @@ int lcv_validate_resident_dev(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot
  * pipeline for b (at most 65536 updates) on the two HIP streams of work-space slot `slot` (0..7) and
  * returns without waiting; lcv_slot_wait waits for that slot and copies the first n verdicts / reason
  * codes out (either pointer may be NULL).  A slot's next batch starts on the device after its previous
- * one; alternate the slots and wait for a slot before reading or reusing it. */
+ * one; alternate the slots and wait for a slot before reading or reusing it.  Synchronous calls use
+ * slot 0 (and, for batches of several 64k chunks, every slot): wait for pending slots before them. */
 int lcv_validate_resident_async(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot,
                                 const uint8_t* genesis_validators_root, int slot);
 int lcv_slot_wait(lcv_ctx* ctx, int slot, uint64_t n, uint8_t* verdict_out, uint8_t* reason_out);
