@@ -278,7 +278,7 @@ class Program:
     def encode(self):
         """hdr: 4 u32 per round (wave-uniform):
              w0 = K | nadd << 4 | mflag << 6 | x2 << 7 | y2 << 8 | neg << 9 | inv << 10 | load << 11 |
-                  emit << 12 | shadow << 13 | red << 16 | used << 24
+                  emit << 12 | shadow << 13 | m12 << 14 | red << 16 | used << 24  (m12: every m X < 2^384)
              w1 = record offset (u32 words), w2 = record words per lane, w3 = 0
            rec: per lane (T lanes per round; lanes >= used: dst = SLOT_NONE):
              r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;
@@ -293,6 +293,9 @@ class Program:
             assert K <= MAXK
             nadd = max(len(o.adds) for o in ops)
             mflag = any(abs(m) != 1 for o in ops for _, _, m in o.prods)
+            # m X < 2^384 for every product of the round (terms <= p, 2^384 / p = 9.85): the scaled
+            # operand keeps 12 words and the product scan stays 12 x 12
+            m12 = mflag and all(abs(m) * len(x) <= 9 for o in ops for x, _, m in o.prods)
             x2 = any(len(x) == 2 for o in ops for x, _, _ in o.prods)
             y2 = any(len(y) == 2 for o in ops for _, y, _ in o.prods)
             neg = any(t.neg for o in ops for x, y, _ in o.prods for t in x + y)
@@ -304,7 +307,8 @@ class Program:
             red = max(self.red_steps(o) for o in ops)
             words = 4 + 3 * K
             hdr += [K | nadd << 4 | int(mflag) << 6 | int(x2) << 7 | int(y2) << 8 | int(neg) << 9 | int(inv) << 10 |
-                    int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | red << 16 | len(ops) << 24,
+                    int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | int(m12) << 14 | red << 16 |
+                    len(ops) << 24,
                     len(rec), words, 0]
             for lane in range(self.team):
                 w = [0] * words
@@ -379,7 +383,7 @@ class Program:
                         X *= m
                     else:
                         assert m == 1
-                    assert X < (1 << 416) and Y < (1 << 384)
+                    assert X < (1 << (384 if (w0 >> 14) & 1 else 416)) and Y < (1 << 384)
                     acc += X * Y
                 for j in range(nadd):
                     s, c = w[2 + j] & SLOT_MASK, w[2 + j] >> 16
