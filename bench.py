@@ -9,14 +9,14 @@ aggregation, Miller loop, final exponentiation, verdicts).  Inputs are resident 
 once, outside the timed region); for N > 1 each step ends with an RCCL all-gather of the per-rank
 verdict bytes (the only collective of the design).  Weak scaling: every rank owns `--n` updates.
 
-Default shape (--depth 4): the serving loop keeps four batches in flight — four resident batches of
+Default shape (--depth 8): the serving loop keeps eight batches in flight — eight resident batches of
 `--n` updates rotate over the work-space slots of the context (lcv_validate_resident_async), so later
 batches' latency-bound early stages (SSWU, hash_to_G2) share the GPU with earlier batches' Miller loop
 and final exponentiation; each timed step is one whole batch, waited for and its verdicts read (or
 all-gathered) inside the timed region.  --depth 1 times one batch at a time; both rates are reported.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n UPDATES_PER_GPU] [--participation full|random]
-                    [--depth 1..4]
+                    [--depth 1..8]
 """
 from __future__ import annotations
 
@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "light-client-consensus-specs_amd"))
 
 import numpy as np  # noqa: E402
 
-DEFAULT_DEPTH = 4
+DEFAULT_DEPTH = 8
 # one HIP stream pair per work-space slot: with HIP's default of 4 hardware queues per process the
 # streams of several slots would share queues (ordering more than the events require); gpurun allows <= 32
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
