@@ -396,6 +396,10 @@ constexpr int32_t kM30 = 0x3FFFFFFF;
 // the additions of f to odd g cancel up to min(eta + 1, remaining, 12) low bits at once)
 LCV_FN int32_t by_divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
+  // f^-1 mod 2^12 by Newton (f odd: f * f = 1 mod 8); f only changes on a swap
+  uint32_t x = f;
+  x *= 2u - f * x;
+  x *= 2u - f * x;
   int i = 30;
   for (;;) {
     const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));
@@ -411,12 +415,12 @@ LCV_FN int32_t by_divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) 
       tmp = f; f = g; g = 0u - tmp;
       tmp = u; u = q; q = 0u - tmp;
       tmp = v; v = r; r = 0u - tmp;
+      x = f;
+      x *= 2u - f * x;
+      x *= 2u - f * x;
     }
     const int limit = (eta + 1) > i ? i : (eta + 1);
     const uint32_t m = (0xFFFFFFFFu >> (32 - limit)) & 0xFFFu;
-    uint32_t x = f;                 // f^-1 mod 2^12 by Newton (f odd: f * f = 1 mod 8)
-    x *= 2u - f * x;
-    x *= 2u - f * x;
     const uint32_t w = (0u - g * x) & m;  // g + w f = 0 mod 2^min(limit, 12)
     g += f * w;
     q += u * w;
