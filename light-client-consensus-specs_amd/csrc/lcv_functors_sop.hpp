@@ -18,6 +18,7 @@ enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_V
 struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
+  static constexpr uint32_t WAVES = 4;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
@@ -88,6 +89,7 @@ struct F_sop_lines {
 
 struct F_sop_acc {
   Work W; SopView P;
+  static constexpr uint32_t WAVES = 4;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -113,6 +115,7 @@ struct F_sop_acc {
 
 struct F_sop_fexp {
   Work W; SopView P;
+  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -153,6 +156,7 @@ struct F_sop_fexp {
 // formulas), affine H(m) -> W.qh and its identity flag -> W.qh_inf
 struct F_sop_h2c {
   Work W; SopView P;
+  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
@@ -186,7 +190,7 @@ struct F_sop_h2c {
 template <class F>
 // LDS is dynamic (sized at launch): with a static size the compiler derives its occupancy target from
 // a smaller LDS than gfx950's 160 KB and gives the kernel 256 VGPRs (2 waves/SIMD).
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_sop(F f, uint32_t n) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) void k_sop(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
   extern __shared__ uint32_t lds[];
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
