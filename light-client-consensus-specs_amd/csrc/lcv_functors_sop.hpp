@@ -18,7 +18,7 @@ enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_V
 struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
-  static constexpr uint32_t WAVES = 4;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
@@ -89,7 +89,7 @@ struct F_sop_lines {
 
 struct F_sop_acc {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 4;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
