@@ -23,8 +23,10 @@ struct Prog {
   uint32_t nhdr, nrec, rounds, slots, nconst, team, items, io_words;
 };
 
-template <uint32_t T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_trace(lcv::SopView P, uint32_t n,
+// W: the program's VGPR budget in waves per SIMD (F::WAVES in csrc/lcv_functors_sop.hpp); the 2-wave
+// programs scan products three at a time, as k_sop does
+template <uint32_t T, uint32_t W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_trace(lcv::SopView P, uint32_t n,
                                                                                       uint32_t lds_words, uint32_t* io,
                                                                                       uint32_t io_words, uint64_t* trace,
                                                                                       uint32_t* hwid) {
@@ -48,7 +50,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const uint32_t h0 = __builtin_amdgcn_readfirstlane(P.hdr[4 * r]);
     const uint32_t off = __builtin_amdgcn_readfirstlane(P.hdr[4 * r + 1]);
     const uint32_t words = __builtin_amdgcn_readfirstlane(P.hdr[4 * r + 2]);
-    if (active) lcv::sop_exec(h0, P.rec + off + lane * words, my, my, lds, P.nslots, io_item, io_item);
+    if (active) lcv::sop_exec<W == 2>(h0, P.rec + off + lane * words, my, my, lds, P.nslots, io_item, io_item);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   }
 }
 
-template <uint32_t T>
+template <uint32_t T, uint32_t W>
 void run(const Prog& pg) {
   auto up = [](const uint32_t* h, size_t n) {
     uint32_t* d;
@@ -81,10 +83,10 @@ void run(const Prog& pg) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  hipLaunchKernelGGL(k_trace<T>, dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace, hw);
+  hipLaunchKernelGGL((k_trace<T, W>), dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace, hw);
   hipDeviceSynchronize();
   hipEventRecord(a);
-  hipLaunchKernelGGL(k_trace<T>, dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace, hw);
+  hipLaunchKernelGGL((k_trace<T, W>), dim3(blocks), dim3(64), lds_bytes, 0, P, pg.items, lds_words, io, pg.io_words, trace, hw);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -185,9 +187,9 @@ void run(const Prog& pg) {
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 10000;
   const uint32_t line_words = 2 * 6 * LCV_SOP_LINES_NSTEPS * 12;
-  run<LCV_SOP_LINES_TEAM>(PROG(lines, LINES, n, line_words));
-  run<LCV_SOP_MILLER_ACC_TEAM>(PROG(miller_acc, MILLER_ACC, n, line_words));
-  run<LCV_SOP_FEXP_TEAM>(PROG(fexp, FEXP, n, 12));
-  run<LCV_SOP_H2C_TEAM>(PROG(h2c, H2C, n, 12));
+  run<LCV_SOP_LINES_TEAM, 3>(PROG(lines, LINES, n, line_words));
+  run<LCV_SOP_MILLER_ACC_TEAM, 2>(PROG(miller_acc, MILLER_ACC, n, line_words));
+  run<LCV_SOP_FEXP_TEAM, 2>(PROG(fexp, FEXP, n, 12));
+  run<LCV_SOP_H2C_TEAM, 2>(PROG(h2c, H2C, n, 12));
   return 0;
 }
