@@ -130,6 +130,14 @@ int lcv_validate_resident_dev(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot
 int lcv_validate_resident_async(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot,
                                 const uint8_t* genesis_validators_root, int slot);
 int lcv_slot_wait(lcv_ctx* ctx, int slot, uint64_t n, uint8_t* verdict_out, uint8_t* reason_out);
+/* Host-input serving entry (the per-batch form of lcv_validate_updates; callers sync-protocol.md:512 per
+ * update and the gossip / Req/Resp ingress p2p-interface.md:69,99 per batch): the batch (at most 65536
+ * updates) is copied into slot `slot`'s pinned staging buffer, uploaded by one DMA on the slot's stream
+ * (overlapping the other slots' kernels), validated, and its verdicts / reasons copied back to pinned
+ * memory — all enqueued without waiting; lcv_slot_wait(slot) waits and copies them out.  The caller's
+ * buffers may be reused as soon as the call returns. */
+int lcv_validate_async(lcv_ctx* ctx, const lcv_update_batch* batch, uint64_t current_slot,
+                       const uint8_t* genesis_validators_root, int slot);
 /* multi-GPU form of lcv_slot_wait: after slot `slot`'s batch (n <= per_rank rows), all-gather every rank's
  * verdict bytes over RCCL (rank-major, each slice zero padded to per_rank) into verdict_all_out
  * (nranks * per_rank bytes) and wait.  Collective: every rank calls it in the same order. */
@@ -151,6 +159,8 @@ const char* lcv_stage_name(int stage);
 int lcv_comm_unique_id(uint8_t* id128);
 int lcv_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id128);
 int lcv_comm_destroy(lcv_ctx* ctx);
+/* ranks in the communicator as RCCL reports them (ncclCommCount) */
+int lcv_comm_count(lcv_ctx* ctx, int* nranks_out);
 /* validate this rank's resident shard (n <= per_rank), all-gather every rank's per_rank verdict bytes
  * (zero padded) into verdict_all_out (nranks * per_rank bytes, rank-major) */
 int lcv_validate_sharded(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot, const uint8_t* genesis_validators_root,
@@ -209,6 +219,8 @@ int lcv_sign_batch(lcv_ctx* ctx, const uint8_t* sk32, const uint8_t* msg32, uint
 /* field ops on (a, b) < p: out per item = a*b, a+b, a-b, a^-1, sqrt_fp2(a + b u) (2 x 48); ok = sqrt exists */
 /* test hook: rows per validate chunk (multiple of 64, <= 65536; default 65536) */
 int lcv_debug_set_chunk(lcv_ctx* ctx, uint64_t rows);
+/* test hook: HIP events held by the context's stage-timing pool (bounded under asynchronous calls) */
+int lcv_debug_event_pool(lcv_ctx* ctx, uint64_t* events_out);
 int lcv_debug_fp(lcv_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint64_t n, uint8_t* out288, uint8_t* ok);
 /* a^((p+1)/4) || a^((p-3)/4) (2 x 48 B) for a < p: the windowed sqrt exponentiations of decompression / SSWU */
 int lcv_debug_fp_pow(lcv_ctx* ctx, const uint8_t* a48, uint64_t n, uint8_t* out96);

@@ -68,6 +68,11 @@ static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id);
 static void be_comm_destroy(lcv_ctx* ctx);
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank);
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout);
+static int be_comm_count(lcv_ctx* ctx, int* out);
+static int be_host_alloc(lcv_ctx* ctx, void** p, size_t bytes);
+static void be_host_free(lcv_ctx* ctx, void* p);
+static int be_wait_event(lcv_ctx* ctx, int ev);
+static size_t be_event_pool_size(lcv_ctx* ctx);
 
 #include "lcv_driver.inc"
 #include "lcv_launch.hpp"
@@ -131,6 +136,27 @@ static void be_free(lcv_ctx* ctx, void* p) {
 static int be_h2d(lcv_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (!bytes) return LCV_OK;
   HIPCHK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cur_stream(ctx)));
+  return LCV_OK;
+}
+// pinned host memory (the staging buffers of lcv_validate_async): copies from it are DMA, asynchronous
+// to the host, so a batch's upload overlaps the kernels of the other slots
+static int be_host_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
+  HIPCHK(ctx, hipSetDevice(ctx->be.device));
+  hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(ctx, LCV_ENOMEM, std::string("hipHostMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  }
+  return LCV_OK;
+}
+static void be_host_free(lcv_ctx* ctx, void* p) {
+  if (!p) return;
+  (void)hipSetDevice(ctx->be.device);
+  (void)hipHostFree(p);
+}
+// the host waits for the active slot's event `ev` (returns at once if it was never recorded)
+static int be_wait_event(lcv_ctx* ctx, int ev) {
+  HIPCHK(ctx, hipEventSynchronize(ctx->be.ev[ctx->be.base / 2][ev]));
   return LCV_OK;
 }
 static int be_d2h(lcv_ctx* ctx, void* dst, const void* src, size_t bytes) {
@@ -217,7 +243,9 @@ static hipEvent_t take_event(lcv_ctx* ctx) {
   return b.pool[b.used++];
 }
 // stage marks: HIP events on the stream the stage's kernels are launched on
+static size_t be_event_pool_size(lcv_ctx* ctx) { return ctx->be.pool.size(); }
 static void be_stage_begin(lcv_ctx* ctx, int stage) {
+  if (ctx->marks_off) return;
   hipEvent_t e = take_event(ctx);
   if (!e) return;
   const int k = ctx->be.base + ctx->be.cur;
@@ -226,6 +254,7 @@ static void be_stage_begin(lcv_ctx* ctx, int stage) {
   ctx->be.open_ev[k] = e;
 }
 static void be_stage_end(lcv_ctx* ctx, int stage) {
+  if (ctx->marks_off) return;
   const int k = ctx->be.base + ctx->be.cur;
   if (ctx->be.open_stage[k] != stage || !ctx->be.open_ev[k]) return;
   hipEvent_t e = take_event(ctx);
@@ -283,6 +312,13 @@ static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, s
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
   ncclResult_t r = ncclAllGather(send, recv, per_rank, ncclUint8, ctx->be.comm, cur_stream(ctx));
   return r == ncclSuccess ? LCV_OK : nccl_fail(ctx, r, "ncclAllGather");
+}
+static int be_comm_count(lcv_ctx* ctx, int* out) {
+  int c = 0;
+  ncclResult_t r = ncclCommCount(ctx->be.comm, &c);
+  if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclCommCount");
+  *out = c;
+  return LCV_OK;
 }
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   HIPCHK(ctx, hipSetDevice(ctx->be.device));

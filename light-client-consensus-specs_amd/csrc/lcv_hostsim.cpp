@@ -68,6 +68,11 @@ static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id);
 static void be_comm_destroy(lcv_ctx* ctx);
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank);
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout);
+static int be_comm_count(lcv_ctx* ctx, int* out);
+static int be_host_alloc(lcv_ctx* ctx, void** p, size_t bytes);
+static void be_host_free(lcv_ctx*, void* p) { free(p); }
+static int be_wait_event(lcv_ctx*, int) { return 0; }
+static size_t be_event_pool_size(lcv_ctx*) { return 0; }
 
 #include "lcv_driver.inc"
 
@@ -81,6 +86,7 @@ static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
   return *p ? LCV_OK : fail(ctx, LCV_ENOMEM, "hostsim: out of memory");
 }
 static void be_free(lcv_ctx*, void* p) { free(p); }
+static int be_host_alloc(lcv_ctx* ctx, void** p, size_t bytes) { return be_alloc(ctx, p, bytes); }
 static int be_h2d(lcv_ctx*, void* dst, const void* src, size_t bytes) { memcpy(dst, src, bytes); return LCV_OK; }
 static int be_d2h(lcv_ctx*, void* dst, const void* src, size_t bytes) { memcpy(dst, src, bytes); return LCV_OK; }
 static int be_d2d(lcv_ctx*, void* dst, const void* src, size_t bytes) { memmove(dst, src, bytes); return LCV_OK; }
@@ -125,6 +131,7 @@ template <class F> static int be_launch_sop(lcv_ctx*, const F& f, uint32_t n) {
 }
 
 static void be_stage_begin(lcv_ctx* ctx, int stage) {
+  if (ctx->marks_off) return;
   Backend& b = ctx->be;
   b.open_stage[b.cur] = stage;
   b.t0[b.cur] = std::chrono::steady_clock::now();
@@ -133,6 +140,7 @@ static void be_stage_begin(lcv_ctx* ctx, int stage) {
 #endif
 }
 static void be_stage_end(lcv_ctx* ctx, int stage) {
+  if (ctx->marks_off) return;
   Backend& b = ctx->be;
   if (b.open_stage[b.cur] != stage) return;
   const auto t1 = std::chrono::steady_clock::now();
@@ -191,6 +199,10 @@ static int comm_exchange(lcv_ctx* ctx, const void* mine, size_t bytes, uint8_t* 
 }
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank) {
   return comm_exchange(ctx, send, per_rank, recv);
+}
+static int be_comm_count(lcv_ctx* ctx, int* out) {
+  *out = ctx->be.comm_n;
+  return LCV_OK;
 }
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   std::vector<double> all((size_t)ctx->be.comm_n);

@@ -64,6 +64,9 @@ SIGNATURES = {
     "lcv_validate_resident_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u8p, C.c_int]),
     "lcv_slot_wait": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, u8p, u8p]),
     "lcv_slot_allgather": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64, u8p]),
+    "lcv_validate_async": (C.c_int, [C.c_void_p, C.POINTER(UpdateBatch), C.c_uint64, u8p, C.c_int]),
+    "lcv_comm_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    "lcv_debug_event_pool": (C.c_int, [C.c_void_p, u64p]),
     "lcv_debug_set_chunk": (C.c_int, [C.c_void_p, C.c_uint64]),
     "lcv_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
     "lcv_set_pipeline": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),

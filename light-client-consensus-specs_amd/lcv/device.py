@@ -200,6 +200,23 @@ class Verifier:
         self._check(self.lib.lcv_validate_resident_async(self.ctx, rb.handle, int(current_slot), ptr(gvr), int(slot)),
                     "lcv_validate_resident_async")
 
+    def validate_async(self, batch: PackedUpdates, current_slot: int, genesis_validators_root: bytes,
+                       slot: int) -> None:
+        """Host-input serving entry (lcv_validate_async): the batch is staged into slot 0..7's pinned buffer,
+        uploaded, validated and its verdicts copied back, all enqueued; collect them with slot_wait(slot).
+        The batch's arrays may be reused as soon as this returns."""
+        b, keep = batch.to_c()
+        gvr = as_u8(bytes(genesis_validators_root))
+        self._check(self.lib.lcv_validate_async(self.ctx, C.byref(b), int(current_slot), ptr(gvr), int(slot)),
+                    "lcv_validate_async")
+        del keep
+
+    def event_pool(self) -> int:
+        """HIP events held for stage timings (test hook: must stay bounded under asynchronous calls)."""
+        n = C.c_uint64()
+        self._check(self.lib.lcv_debug_event_pool(self.ctx, C.byref(n)), "lcv_debug_event_pool")
+        return int(n.value)
+
     def slot_wait(self, slot: int, n: int, verdict: Optional[np.ndarray] = None, reason: Optional[np.ndarray] = None):
         """Wait for the batch of `slot`; its first n verdicts (bool) and reason codes."""
         v = verdict if verdict is not None else np.zeros(n, np.uint8)

@@ -6,8 +6,8 @@ collective is one all-gather of the per-update verdict bytes — RCCL over xGMI,
 device buffer, inside liblcv.so (`lcv_validate_sharded`).  No data-path exchange.
 
 Rendezvous: rank 0 creates the 128-byte RCCL unique id (`lcv_comm_unique_id`) and publishes it in a
-file that the other ranks of the same launch (same parent process, same MASTER_PORT: all on one node)
-poll for.  The test suite runs the same code on the host simulation, whose stand-in collective
+file keyed on the launch's MASTER_ADDR:MASTER_PORT (all ranks on one node), tagged with a token unique
+to the launch (`launch_tag`), which the other ranks poll for.  The test suite runs the same code on the host simulation, whose stand-in collective
 exchanges files (tests/test_multi.py).
 """
 from __future__ import annotations
@@ -30,16 +30,45 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _proc_start(pid: int) -> str:
+    """Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), '' if unknown."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[19]
+    except (OSError, IndexError):
+        return ""
+
+
+def launch_tag() -> str:
+    """A token that every rank of ONE launch computes identically and no other launch does:
+    LCV_RDZV_KEY (set by bench.py's own spawner or by a caller), else the launcher's run id
+    (TORCHELASTIC_RUN_ID, when not the static default "none"), else the shared parent process's pid and
+    start time (the ranks of torch.distributed.run / bench.py --gpus are children of one launcher)."""
+    tag = os.environ.get("LCV_RDZV_KEY")
+    if tag:
+        return tag
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    if run and run != "none":
+        return f"run:{run}"
+    ppid = os.getppid()
+    return f"ppid:{ppid}:{_proc_start(ppid)}"
+
+
 def _id_path(key: Optional[str]) -> str:
+    """Rendezvous file: keyed on the launch's MASTER_ADDR:MASTER_PORT (not on the parent pid)."""
     if key is None:
-        key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+        key = f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}_{os.environ.get('MASTER_PORT', '0')}"
     d = os.environ.get("LCV_RENDEZVOUS_DIR", tempfile.gettempdir())
-    return os.path.join(d, f"lcv_rccl_id_{key}")
+    safe = "".join(c if c.isalnum() or c in "._-" else "_" for c in key)
+    return os.path.join(d, f"lcv_rccl_id_{safe}")
 
 
 def rendezvous(lib, rank: int, world: int, key: Optional[str] = None, timeout: float = 300.0) -> bytes:
-    """The communicator id, made by rank 0 and read by every other rank of this launch."""
+    """The communicator id, made by rank 0 and read by every other rank of this launch.  The file holds
+    the id and this launch's tag (launch_tag()); a rank accepts only a file carrying its own tag, so a
+    file left behind by an earlier launch on the same address and port is never used."""
     path = _id_path(key)
+    tag = launch_tag().encode()
     if rank == 0:
         uid = np.zeros(128, np.uint8)
         rc = lib.lcv_comm_unique_id(ptr(uid))
@@ -47,7 +76,7 @@ def rendezvous(lib, rank: int, world: int, key: Optional[str] = None, timeout: f
             raise LcvError(f"lcv_comm_unique_id failed with status {rc}")
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "wb") as f:
-            f.write(uid.tobytes())
+            f.write(uid.tobytes() + tag)
         os.replace(tmp, path)  # atomic: readers see the whole id or nothing
         return uid.tobytes()
     t0 = time.monotonic()
@@ -55,12 +84,12 @@ def rendezvous(lib, rank: int, world: int, key: Optional[str] = None, timeout: f
         try:
             with open(path, "rb") as f:
                 b = f.read()
-            if len(b) == 128:
-                return b
+            if len(b) == 128 + len(tag) and b[128:] == tag:
+                return b[:128]
         except FileNotFoundError:
             pass
         if time.monotonic() - t0 > timeout:
-            raise LcvError(f"rendezvous: no communicator id at {path} after {timeout:.0f} s")
+            raise LcvError(f"rendezvous: no communicator id for launch {tag.decode()} at {path} after {timeout:.0f} s")
         time.sleep(0.01)
 
 
@@ -90,6 +119,12 @@ class Comm:
         self.v._check(self.v.lib.lcv_slot_allgather(self.v.ctx, int(slot), int(n), int(per_rank), ptr(buf)),
                       "lcv_slot_allgather")
         return buf
+
+    def count(self) -> int:
+        """Ranks in the communicator as RCCL reports them (ncclCommCount)."""
+        c = C.c_int()
+        self.v._check(self.v.lib.lcv_comm_count(self.v.ctx, C.byref(c)), "lcv_comm_count")
+        return int(c.value)
 
     def allreduce_max(self, x: float) -> float:
         d = C.c_double(float(x))

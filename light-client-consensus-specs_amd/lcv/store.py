@@ -169,6 +169,13 @@ def process_light_client_updates(store, updates: Sequence, current_slot: int, ge
     """Sequential `process_light_client_update` over `updates` (in order) with batched GPU
     validation; returns accept flags.  `reasons_out` (optional list) receives each update's
     validation reason code (0 = valid, REASONS in lcv.sync_protocol) under the store it met."""
+    v = verifier if verifier is not None else runtime.default_verifier()
+    if v.config != config.active():
+        # the host-side periods / UPDATE_TIMEOUT read config.active(); the device checks read v.config
+        raise ValueError(f"process_light_client_updates: the verifier validates under network configuration "
+                         f"{v.config.name!r} but lcv.config.active() is {config.active().name!r}; call "
+                         f"lcv.config.set_active() (or Verifier.set_config) so both sides agree")
+    verifier = v
     n = len(updates)
     accepted = np.zeros(n, bool)
     reasons = np.zeros(n, np.uint8)

@@ -3,13 +3,32 @@ verdicts and reasons equal the synchronous call's and the rows' construction."""
 import numpy as np
 import pytest
 
-from test_pipeline_hostsim import check_async_slots
+from test_pipeline_hostsim import check_async_slots, check_host_async
 
 pytestmark = pytest.mark.gpu
 
 
 def test_async_slots_gpu(gpu_verifier):
     check_async_slots(gpu_verifier)
+
+
+def test_host_async_gpu(gpu_verifier):
+    """lcv_validate_async (pinned staging, DMA upload, pinned verdicts) on eight slots, plus the bounded
+    stage-timing event pool under 50 asynchronous batches."""
+    v = gpu_verifier
+    check_host_async(v, cycles=3)
+    from test_pipeline_hostsim import _two_batches
+    a, _ = _two_batches(v, 64)
+    v.set_store(a.store_finalized_slot, a.current.ssz, a.next.ssz)
+    rb = v.upload(a.updates)
+    before = v.event_pool()
+    for k in range(50):
+        v.validate_resident_async(rb, a.current_slot, a.genesis_validators_root, k % 8)
+        if k >= 7:
+            v.slot_wait((k + 1) % 8, a.updates.n)
+    for s in range(8):
+        v.slot_wait(s, a.updates.n)
+    assert v.event_pool() == before
 
 
 def test_async_slots_full_batches_gpu(gpu_verifier):

@@ -1,5 +1,7 @@
 """The slice pipeline of validate (lcv_set_pipeline) on the host simulation: the slicing of the batch
 and of the work space (work_view) must not change any verdict or reason (CPU, no GPU)."""
+import copy
+
 import numpy as np
 import pytest
 
@@ -65,8 +67,49 @@ def check_async_slots(v):
     assert np.array_equal(again[1], sync_a[1])
 
 
+def check_host_async(v, cycles=3):
+    """lcv_validate_async (host batch in, verdicts out, eight in flight): every batch's verdicts and
+    reasons equal its construction and the synchronous call's; the caller's arrays are reusable when the
+    call returns (overwritten before the slot is waited for); mixing with resident async calls on the
+    same slot keeps each call's results; the stage-timing event pool stays bounded."""
+    a, b = _two_batches(v)
+    v.set_store(a.store_finalized_slot, a.current.ssz, a.next.ssz)
+    sync_a = v.validate(a.updates, a.current_slot, a.genesis_validators_root)
+    pool0 = v.event_pool()
+    for rep in range(cycles):
+        for s in range(8):
+            x = a if (s + rep) % 2 == 0 else b
+            if rep == 1 and s == 3:  # the call copied the batch: clobbering the caller's arrays is harmless
+                tmp = copy.deepcopy(x.updates)
+                v.validate_async(tmp, x.current_slot, x.genesis_validators_root, s)
+                tmp.sync_signature[:] = 0
+                tmp.att_beacon[:] = 0xFF
+            else:
+                v.validate_async(x.updates, x.current_slot, x.genesis_validators_root, s)
+        for s in range(8):
+            x = a if (s + rep) % 2 == 0 else b
+            ok, r = v.slot_wait(s, x.updates.n)
+            assert np.array_equal(r, x.expected_reason) and np.array_equal(ok.astype(bool), r == 0)
+            if x is a:
+                assert np.array_equal(r, sync_a[1])
+    # a resident async batch on a slot after a host-input one (and back) reports its own results
+    rb = v.upload(b.updates)
+    v.validate_async(a.updates, a.current_slot, a.genesis_validators_root, 2)
+    assert np.array_equal(v.slot_wait(2, a.updates.n)[1], a.expected_reason)
+    v.validate_resident_async(rb, b.current_slot, b.genesis_validators_root, 2)
+    assert np.array_equal(v.slot_wait(2, b.updates.n)[1], b.expected_reason)
+    v.validate_async(a.updates, a.current_slot, a.genesis_validators_root, 2)
+    assert np.array_equal(v.slot_wait(2, a.updates.n)[1], a.expected_reason)
+    # asynchronous calls take no stage-timing events (ADVICE r02: the pool grew ~24 events per batch)
+    assert v.event_pool() <= max(pool0, 64)
+
+
 def test_async_slots_hostsim():
     check_async_slots(H.hostsim_verifier())
+
+
+def test_host_async_hostsim():
+    check_host_async(H.hostsim_verifier(), cycles=2)
 
 
 def test_async_rejects_bad_slot():

@@ -25,3 +25,15 @@ def test_is_better_update_prefers_supermajority_and_older_data():
     assert LS.is_better_update(upd(400, 100, 101), upd(400, 100, 101, False))  # finality present
     assert LS.is_better_update(upd(400, 90, 101), upd(400, 100, 101))       # older attested data
     assert LS.is_better_update(upd(400, 100, 101), upd(400, 100, 102))      # older signature slot
+
+
+def test_store_refuses_config_mismatch():
+    """the host-side store logic reads lcv.config.active(), the device checks the verifier's
+    configuration; a verifier set to another network than the active one is refused, not half-applied."""
+    import pytest
+    from lcv import config
+    from lcv import store as LS
+    v = H.hostsim_verifier()
+    v.set_config(config.TESTNET)
+    with pytest.raises(ValueError, match="network configuration"):
+        LS.process_light_client_updates(None, [], 0, bytes(32), verifier=v)

@@ -47,8 +47,9 @@ def test_opcount_every_stage():
     for st in ("h2c_sswu", "hash_to_g2", "sig_decode", "miller_lines_sig", "g1_aggregate", "miller_lines",
                "miller_loop", "final_exp"):
         assert per.get(st, {}).get("fp_mul", 0) > 0, st
-    for st in ("pre_checks", "nsc_htr"):
-        assert per[st]["sha"] > 0
+    assert per["pre_checks"]["sha"] > 0
+    # HTR(SyncCommittee) is charged per distinct committee: 1,025 SHA-256 calls = 2,050 compressions
+    assert "nsc_htr" not in per and c["per_committee"]["nsc_htr"]["sha"] == 2050
     # the SOP programs' products and reductions are what the op counter sees (padding products excluded):
     # each is half of a reduced Fp multiplication
     import gen_sop as GS

@@ -35,21 +35,27 @@ def count(n: int = 8, participation: str = "full", npool: int = 1) -> dict:
     names = list(v.last_timings().keys())
     buf = (C.c_ulonglong * (4 * len(names)))()
     lib.dll.lcv_debug_opcounts(v.ctx, buf, len(names))
-    per = {}
+    per, per_comm = {}, {}
     for s, name in enumerate(names):
         # an SOP half-multiplication (a 12x12-limb product or a Montgomery reduction) is half of a
         # reduced Fp multiplication's 288 multiply-accumulates
         fm, fa, sh = buf[4 * s] + buf[4 * s + 3] / 2, buf[4 * s + 1], buf[4 * s + 2]
-        if fm or fa or sh:
-            per[name] = {"fp_mul": fm / n, "fp_add": fa / n, "sha": sh / n,
-                         "int32_ops": (600 * fm + 24 * fa + 2100 * sh) / n}
+        if not (fm or fa or sh):
+            continue
+        # HTR(next_sync_committee) runs once per DISTINCT committee of the batch's pool, not per update
+        units, dst = (npool, per_comm) if name == "nsc_htr" else (n, per)
+        dst[name] = {"fp_mul": fm / units, "fp_add": fa / units, "sha": sh / units,
+                     "int32_ops": (600 * fm + 24 * fa + 2100 * sh) / units}
     tot = {k: sum(d[k] for d in per.values()) for k in ("fp_mul", "fp_add", "sha")}
-    pool = "nsc pool of 1: HTR(next_sync_committee) amortised over the batch" if npool == 1 else \
-        f"{npool} distinct next_sync_committee values"
-    return {"config": f"{n} synthetic Deneb updates, {participation} participation, all branches ({pool})",
+    return {"config": f"{n} synthetic Deneb updates, {participation} participation, all branches, {npool} distinct "
+                      f"next_sync_committee value(s)",
+            "counted": "executed: the device's own operations (host-simulation build of the kernel code); an SOP "
+                       "op of K products + one reduction counts (K + 1) / 2 Fp multiplications",
             "op_model": "INT32 ops = 600*fp_mul + 24*fp_add + 2100*sha (SURVEY.md 8(d))",
-            "per_update": per, "total_per_update": tot,
-            "int32_ops_per_update": 600 * tot["fp_mul"] + 24 * tot["fp_add"] + 2100 * tot["sha"]}
+            "per_update": per, "per_committee": per_comm, "total_per_update": tot,
+            "int32_ops_per_update": 600 * tot["fp_mul"] + 24 * tot["fp_add"] + 2100 * tot["sha"],
+            "note": "total_per_update excludes per_committee stages: a batch of n updates with npool distinct "
+                    "committees costs n * per_update + npool * per_committee"}
 
 
 def main():
