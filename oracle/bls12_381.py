@@ -490,6 +490,14 @@ def g2_decompress(data: bytes) -> G2Point:
 
 
 # ----------------------------------------------------------------------------- hash_to_G2 (RFC 9380)
+SHA_COMPRESSIONS = [0]  # op counter (oracle/canonical.py): compressions of expand_message_xmd's SHA-256 calls
+
+
+def _sha256(data: bytes) -> bytes:
+    SHA_COMPRESSIONS[0] += (len(data) + 8) // 64 + 1
+    return hashlib.sha256(data).digest()
+
+
 def expand_message_xmd(msg: bytes, dst: bytes, len_in_bytes: int) -> bytes:
     """RFC 9380 §5.3.1 with SHA-256 (b_in_bytes = 32, s_in_bytes = 64)."""
     b_in, s_in = 32, 64
@@ -499,11 +507,11 @@ def expand_message_xmd(msg: bytes, dst: bytes, len_in_bytes: int) -> bytes:
     dst_prime = dst + bytes([len(dst)])
     z_pad = bytes(s_in)
     l_i_b = len_in_bytes.to_bytes(2, "big")
-    b0 = hashlib.sha256(z_pad + msg + l_i_b + b"\x00" + dst_prime).digest()
-    bi = hashlib.sha256(b0 + b"\x01" + dst_prime).digest()
+    b0 = _sha256(z_pad + msg + l_i_b + b"\x00" + dst_prime)
+    bi = _sha256(b0 + b"\x01" + dst_prime)
     out = bytearray(bi)
     for i in range(2, ell + 1):
-        bi = hashlib.sha256(bytes(x ^ y for x, y in zip(b0, bi)) + bytes([i]) + dst_prime).digest()
+        bi = _sha256(bytes(x ^ y for x, y in zip(b0, bi)) + bytes([i]) + dst_prime)
         out += bi
     return bytes(out[:len_in_bytes])
 

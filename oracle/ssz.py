@@ -19,13 +19,19 @@ import sys
 from typing import Any, Dict, List, Tuple
 
 
+# op counter (oracle/canonical.py): SHA-256 compressions of every sha256() call, ceil((len + 9) / 64)
+SHA_COMPRESSIONS = [0]
+
+
 def sha256(data: bytes) -> bytes:
+    SHA_COMPRESSIONS[0] += (len(data) + 8) // 64 + 1
     return hashlib.sha256(data).digest()
 
 
 ZERO_HASHES: List[bytes] = [bytes(32)]
 for _ in range(64):
     ZERO_HASHES.append(sha256(ZERO_HASHES[-1] + ZERO_HASHES[-1]))
+SHA_COMPRESSIONS[0] = 0  # the zero-subtree table is a constant, not per-call work
 
 
 def _next_pow2_depth(n: int) -> int:
