@@ -360,6 +360,51 @@ def g2_mul(p: G2Point, k: int) -> G2Point:
     return r
 
 
+# #E2(Fp2) = H2 * R; H2 = 13^2 * 23^2 * 2713 * 11953 * 262069 * (a 448-bit prime)
+H2 = 0x5D543A95414E7F1091D50792876A202CD91DE4547085ABAA68A205B2E5A7DDFA628F1CB4D9E82EF21537E293A6691AE1616EC6E786F0C70CF1C38E31C7238E5
+H2_SMALL_PRIMES = (13, 23, 2713, 11953, 262069)
+H2_BIG = H2 // (13 ** 2 * 23 ** 2 * 2713 * 11953 * 262069)
+
+
+def _g2_order_dividing(t: G2Point, m: int, primes) -> int:
+    """The order of t, given that it divides m (whose prime factors are `primes`)."""
+    for q in primes:
+        while m % q == 0 and g2_mul(t, m // q) is None:
+            m //= q
+    return m
+
+
+def g2_point_of_order(ell: int, start: int = 2) -> G2Point:
+    """A point of E2(Fp2) of order exactly `ell`, a divisor of H2 built from its primes: a deterministic
+    curve point times #E2 / (ell's primes' full part of #E2), then times primes until the order is ell.
+    Test inputs for the G2 membership test's exceptional cases (tests/test_oracle_bls.py,
+    tests/test_gpu_intermediates.py, tools/gen_sop.py --check)."""
+    n = H2 * R
+    primes = [q for q in H2_SMALL_PRIMES + (H2_BIG,) if ell % q == 0]
+    full = 1
+    for q in primes:
+        while n % (full * q) == 0:
+            full *= q
+    assert full % ell == 0 and ell > 1
+    x = start
+    while x < start + 200:  # (E2's 13- and 23-parts have exponent 13 / 23: no point of order 169 or 529)
+        X = (x, 1)
+        x += 1
+        y = f2_sqrt(f2_add(f2_mul(f2_sqr(X), X), B2))
+        if y is None:
+            continue
+        t = g2_mul((X, y), n // full)
+        if t is None:
+            continue
+        o = _g2_order_dividing(t, full, primes)
+        if o % ell:
+            continue
+        t = g2_mul(t, o // ell)
+        if t is not None and _g2_order_dividing(t, ell, primes) == ell:
+            return t
+    raise ValueError(f"no point of order {ell} found on E2")
+
+
 def g1_in_subgroup(p: G1Point) -> bool:
     return g1_on_curve(p) and g1_mul(p, R) is None
 

@@ -176,3 +176,30 @@ def test_point_encoding_round_trip():
         p1, p2 = B.g1_mul(B.G1_GEN, k), B.g2_mul(B.G2_GEN, k)
         assert B.g1_decompress(B.g1_compress(p1)) == p1
         assert B.g2_decompress(B.g2_compress(p2)) == p2
+
+
+def test_g2_torsion_points():
+    """The E2 points of tests/g2_edge_points.py: on the curve, of the stated order, outside G2 by r*P and
+    by the psi test; order 13 puts the |x| walk at T = -Q before its second addition; no point of E2
+    reaches T = +Q at an addition (gcd(k - 1, #E2) = 1 for every addition prefix k)."""
+    from math import gcd
+    import g2_edge_points as E
+    n = B.H2 * B.R
+    k, prefixes = 1, []
+    for bit in bin(B.X_ABS)[3:]:
+        k *= 2
+        if bit == "1":
+            prefixes.append(k)
+            k += 1
+    assert tuple(prefixes) == E.ADD_PREFIXES and k == B.X_ABS
+    assert all(gcd(p - 1, n) == 1 for p in prefixes)
+    assert [p for p in prefixes if gcd(p + 1, n) > 1] == [12]  # 13 | 12 + 1: only T = -Q is reachable
+    for name, p in E.edge_points().items():
+        assert B.g2_on_curve(p) and p is not None, name
+        assert not B.g2_in_subgroup(p) and not B.g2_in_subgroup_psi(p), name
+        assert B.g2_decompress(B.g2_compress(p)) == p, name
+    o13 = B.g2_point_of_order(13)
+    assert B.g2_mul(o13, 12) == B.g2_neg(o13) and B.g2_mul(o13, 13) is None
+    for ell in (23, 2713, 11953, 262069):
+        q = B.g2_point_of_order(ell)
+        assert B.g2_mul(q, ell) is None and B.g2_mul(q, ell // ell) is not None

@@ -1124,9 +1124,17 @@ def check_miller(lp, ap):
         y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(X), X), B.B2))
         if y is not None:
             cases.append(((X, y), False))
+    # the exceptional path (tests/g2_edge_points.py): points of the cofactor's small
+    # orders (order 13 meets T = -Q before the walk's second addition), G2 + torsion sums
+    g = B.g2_mul(B.G2_GEN, rnd.randrange(1, B.R))
+    for ell in (13, 23, 2713, 11953, 262069):
+        t = B.g2_point_of_order(ell)
+        cases += [(t, False), (B.g2_neg(t), False), (B.g2_add(g, t), False)]
+    cases.append((B.g2_point_of_order(B.H2_BIG), False))
     for q, want in cases:
         assert subgroup_emulated(lp, q) == want == B.g2_in_subgroup(q), "SOP subgroup check mismatch"
-    print("  SOP Miller (lines + accumulation) checked against oracle pairings; fused G2 subgroup check too")
+    print("  SOP Miller (lines + accumulation) checked against oracle pairings; fused G2 subgroup check too "
+          f"({len(cases)} points, incl. small-order / G2 + torsion points)")
 
 
 def check_fexp(fp):
