@@ -147,6 +147,12 @@ int lcv_slot_allgather(lcv_ctx* ctx, int slot, uint64_t n, uint64_t per_rank, ui
  * (default) runs the stages one after another over the whole chunk (per-stage timings available);
  * verdicts are identical either way.  Performance knob only, no reference counterpart. */
 int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
+/* Latency engine for small batches (the reference's per-update usage: validate_light_client_update and
+ * bls.FastAggregateVerify once per update, sync-protocol.md:512, :464): calls whose batch (or chunk) has
+ * at most max_rows rows run signature decoding, the SSWU maps and the pairing / hash_to_G2 programs one
+ * item per workgroup, each Montgomery product spread over a wave's lanes.  Results are identical to the
+ * batch engine's.  Default 32; 0 = batch engine always.  Performance knob only. */
+int lcv_set_latency_mode(lcv_ctx* ctx, uint64_t max_rows);
 /* kernel time of the last validate call: total and per stage (ms); names via lcv_stage_name
  * (stage times are recorded by the serial shape only: zero under a multi-stream pipeline) */
 int lcv_last_timings(lcv_ctx* ctx, float* ms_out, int max_stages, int* nstages);

@@ -144,6 +144,11 @@ class Verifier:
         (overlapping stages of different slices); (1, 1) = serial stages with per-stage timings."""
         self._check(self.lib.lcv_set_pipeline(self.ctx, int(streams), int(chunks)), "lcv_set_pipeline")
 
+    def set_latency_mode(self, max_rows: int) -> None:
+        """Batches of at most max_rows rows use the latency engine (one item per workgroup, products
+        spread over the lanes; identical results); 0 = the batch engine always (default 32)."""
+        self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
+
     def last_timings(self) -> Dict[str, float]:
         ms = (C.c_float * 16)()
         n = C.c_int()
