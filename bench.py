@@ -467,9 +467,23 @@ def latency_lines(v, sb, calls: int = 20) -> dict:
         t0 = time.perf_counter()
         fav_ok &= v.fast_aggregate_verify(pks, msg, sig)
         tf.append(time.perf_counter() - t0)
+    # the same single-update call on the batch engine only (lcv_set_latency_mode(0))
+    v.set_latency_mode(0)
+    try:
+        v.validate(one, sb.current_slot, gvr)
+        tb = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            v.validate(one, sb.current_slot, gvr)
+            tb.append(time.perf_counter() - t0)
+    finally:
+        v.set_latency_mode(32)
     return {"validate_one_update_ms": round(1000 * float(np.median(ts)), 3), "validate_one_update_valid": bool(ok[0]),
+            "validate_one_update_batch_engine_ms": round(1000 * float(np.median(tb)), 3),
             "fast_aggregate_verify_512_ms": round(1000 * float(np.median(tf)), 3),
-            "fast_aggregate_verify_512_cold_ms": round(1000 * first, 3), "fast_aggregate_verify_valid": bool(fav_ok)}
+            "fast_aggregate_verify_512_cold_ms": round(1000 * first, 3), "fast_aggregate_verify_valid": bool(fav_ok),
+            "note": "latency engine on (lcv_set_latency_mode(32), default): signature decoding and the SSWU maps "
+                    "one update per wave, products spread over the lanes; *_batch_engine_ms with it off"}
 
 
 def wire_path(v, sb, n: int) -> dict:

@@ -19,7 +19,6 @@ struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t MAXK = LCV_SOP_LINES_MAXK;  // most products of an op (the latency engine's record size)
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
@@ -91,7 +90,6 @@ struct F_sop_lines {
 struct F_sop_acc {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t MAXK = LCV_SOP_MILLER_ACC_MAXK;  // most products of an op (the latency engine's record size)
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -118,7 +116,6 @@ struct F_sop_acc {
 struct F_sop_fexp {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t MAXK = LCV_SOP_FEXP_MAXK;  // most products of an op (the latency engine's record size)
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -160,7 +157,6 @@ struct F_sop_fexp {
 struct F_sop_h2c {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t MAXK = LCV_SOP_H2C_MAXK;  // most products of an op (the latency engine's record size)
   static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");

@@ -48,9 +48,8 @@ static int be_sync(lcv_ctx* ctx);
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
-// the latency engine's launches run the same per-item / per-round code (the device spreads products over lanes)
+// the latency engine's launches run the same per-item code (the device spreads products over lanes)
 template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch(ctx, f, n); }
-template <class F> static int be_launch_sop_wide(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch_sop(ctx, f, n); }
 static int be_fork(lcv_ctx*) { return 0; }
 static int be_join(lcv_ctx*) { return 0; }
 static void be_use_stream(lcv_ctx* ctx, int k);

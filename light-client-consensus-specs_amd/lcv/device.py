@@ -145,8 +145,9 @@ class Verifier:
         self._check(self.lib.lcv_set_pipeline(self.ctx, int(streams), int(chunks)), "lcv_set_pipeline")
 
     def set_latency_mode(self, max_rows: int) -> None:
-        """Batches of at most max_rows rows use the latency engine (one item per workgroup, products
-        spread over the lanes; identical results); 0 = the batch engine always (default 32)."""
+        """Batches of at most max_rows rows decode signatures and run the SSWU maps on the latency engine
+        (one item per wave, products spread over the lanes; identical results); 0 = the batch engine
+        always (default 32)."""
         self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
 
     def last_timings(self) -> Dict[str, float]:
