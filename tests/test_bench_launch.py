@@ -18,7 +18,8 @@ ARGS = ["--n", "64", "--steps", "2", "--warmup", "1", "--depth", "2", "--quick"]
 
 def _run(extra_env, args, timeout=600):
     H.ensure_hostsim()
-    env = dict(os.environ, LCV_BENCH_HOSTSIM="1", OMP_NUM_THREADS="2")
+    env = dict(os.environ, LCV_BENCH_HOSTSIM="1")
+    env.setdefault("OMP_NUM_THREADS", "2")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LCV_RDZV_KEY"):
         env.pop(k, None)
     env.update(extra_env)
@@ -27,16 +28,17 @@ def _run(extra_env, args, timeout=600):
 
 
 @pytest.mark.timeout(900)
-def test_bench_gpus2_spawns_two_ranks():
-    p = _run({}, ["--gpus", "2"] + ARGS)
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_gpus_n_spawns_n_ranks(world):
+    p = _run({"OMP_NUM_THREADS": "1" if world > 2 else "2"}, ["--gpus", str(world)] + ARGS)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2
+    assert d["n_gpus"] == world and d["rccl_ranks"] == world
     assert d["all_valid"] and d["pcie_inclusive_serving"]["all_valid"]
     assert d["value"] > 0 and "host simulation" in d["library"]
-    assert "[rank 1]" in p.stderr
+    assert all(f"[rank {r}]" in p.stderr for r in range(world))
 
 
 @pytest.mark.timeout(300)
