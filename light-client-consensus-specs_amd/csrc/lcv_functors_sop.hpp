@@ -207,7 +207,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
     const uint32_t h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
     const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 1]);
     const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
-    if (active) lcv::sop_exec<F::WAVES == 2>(h0, f.P.rec + off + lane * words, my, my, lds, ns, io_in, io_out);
+    if (active) lcv::sop_exec(h0, f.P.rec + off + lane * words, my, my, lds, ns, io_in, io_out);
     __syncthreads();
   }
   if (active) f.epilogue(item, lane, my);

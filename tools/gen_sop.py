@@ -43,6 +43,8 @@ R = 1 << 384
 RINV = pow(R, -1, P)
 NP = (-pow(P, -1, R)) % R          # -p^-1 mod R (REDC)
 ACC_BITS = 800                     # 25 x 32-bit accumulator words
+L28, M28 = 28, (1 << 28) - 1       # device limbs: 14 x 28 bits per value, 28 64-bit column accumulators
+NLIMB = 14
 MAXK = 15
 SLOT_MASK = 0xFFF
 NEG = 0x8000                       # term halfword: slot | NEG
@@ -55,6 +57,15 @@ def mont(x):
 
 def unmont(x):
     return x * RINV % P
+
+
+def limb_bounds(v, n=15):
+    """Per-limb bounds of a normalised 28-bit-limb value <= v."""
+    return [min(M28, v >> (L28 * i)) for i in range(n)]
+
+
+TB28 = limb_bounds(P)                                  # a term: a value < p or a shadow p - v in (0, p]
+PL28 = [(P >> (L28 * i)) & M28 for i in range(NLIMB)]  # p's limbs
 
 
 # ============================================================================ program representation
@@ -274,11 +285,37 @@ class Program:
             k += 1
         return k
 
+    # ------------------------------------------------------------ device column bounds (28-bit limbs)
+    @staticmethod
+    def col_bound(op, x15):
+        """Largest 64-bit column accumulator of `op` on the device (csrc/lcv_sop.hpp sop_exec): every
+        operand (a sum of terms, scaled by m) enters the products as normalised 28-bit limbs, so column c
+        receives x_i y_j < 2^56 per limb pair, plus the Montgomery reduction's quotient digits times p's
+        limbs and the carries."""
+        cols = [0] * 28
+        for x, y, m in op.prods:
+            assert m * len(x) * P < 1 << (420 if x15 else 392)
+            bx, by = limb_bounds(m * len(x) * P), limb_bounds(len(y) * P)
+            for i in range(15):
+                for j in range(14):
+                    cols[i + j] += bx[i] * by[j]
+        for i in range(14):
+            qb = M28 if i < 13 else (1 << 20) - 1
+            for j in range(14):
+                cols[i + j] += qb * PL28[j]
+        return max(cols) + (1 << 40)
+
+    def round_flags(self, ops):
+        """x15 of a round (some m X >= 2^392: X takes 15 limbs), checked against the column bound."""
+        x15 = int(any(m * len(x) * P >= 1 << 392 for o in ops for x, _, m in o.prods))
+        assert all(self.col_bound(o, x15) < 1 << 64 for o in ops), f"{self.name}: a column exceeds 2^64"
+        return x15
+
     # ------------------------------------------------------------ encoding
     def encode(self):
         """hdr: 4 u32 per round (wave-uniform):
              w0 = K | nadd << 4 | mflag << 6 | x2 << 7 | y2 << 8 | neg << 9 | inv << 10 | load << 11 |
-                  emit << 12 | shadow << 13 | m12 << 14 | red << 16 | used << 24  (m12: every m X < 2^384)
+                  emit << 12 | shadow << 13 | red << 16 | x15 << 21 | used << 24  (x15: some m X >= 2^392)
              w1 = record offset (u32 words), w2 = record words per lane, w3 = 0
            rec: per lane (T lanes per round; lanes >= used: dst = SLOT_NONE):
              r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;
@@ -293,9 +330,7 @@ class Program:
             assert K <= MAXK
             nadd = max(len(o.adds) for o in ops)
             mflag = any(abs(m) != 1 for o in ops for _, _, m in o.prods)
-            # m X < 2^384 for every product of the round (terms <= p, 2^384 / p = 9.85): the scaled
-            # operand keeps 12 words and the product scan stays 12 x 12
-            m12 = mflag and all(abs(m) * len(x) <= 9 for o in ops for x, _, m in o.prods)
+            x15 = self.round_flags(ops)
             x2 = any(len(x) == 2 for o in ops for x, _, _ in o.prods)
             y2 = any(len(y) == 2 for o in ops for _, y, _ in o.prods)
             neg = any(t.neg for o in ops for x, y, _ in o.prods for t in x + y)
@@ -305,10 +340,11 @@ class Program:
             emit = any(o.emit is not None for o in ops)
             shadow = any(o.dst_shadow is not None or o.load_shadow is not None for o in ops)
             red = max(self.red_steps(o) for o in ops)
+            assert red <= 10, "result above 2^392"
             words = 4 + 3 * K
             hdr += [K | nadd << 4 | int(mflag) << 6 | int(x2) << 7 | int(y2) << 8 | int(neg) << 9 | int(inv) << 10 |
-                    int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | int(m12) << 14 | red << 16 |
-                    len(ops) << 24,
+                    int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | red << 16 |
+                    x15 << 21 | len(ops) << 24,
                     len(rec), words, 0]
             for lane in range(self.team):
                 w = [0] * words
@@ -383,7 +419,7 @@ class Program:
                         X *= m
                     else:
                         assert m == 1
-                    assert X < (1 << (384 if (w0 >> 14) & 1 else 416)) and Y < (1 << 384)
+                    assert X < (1 << (420 if (w0 >> 21) & 1 else 392)) and Y < (1 << 392)
                     acc += X * Y
                 for j in range(nadd):
                     s, c = w[2 + j] & SLOT_MASK, w[2 + j] >> 16
