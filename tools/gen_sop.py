@@ -45,6 +45,7 @@ NP = (-pow(P, -1, R)) % R          # -p^-1 mod R (REDC)
 ACC_BITS = 800                     # 25 x 32-bit accumulator words
 L28, M28 = 28, (1 << 28) - 1       # device limbs: 14 x 28 bits per value, 28 64-bit column accumulators
 NLIMB = 14
+KARATSUBA = True                   # device products: one Karatsuba level where the columns allow
 MAXK = 15
 SLOT_MASK = 0xFFF
 NEG = 0x8000                       # term halfword: slot | NEG
@@ -305,17 +306,34 @@ class Program:
                 cols[i + j] += qb * PL28[j]
         return max(cols) + (1 << 40)
 
+    @staticmethod
+    def kara_bound(op):
+        """Largest column of the Karatsuba middle product M = sum_k (X0 + X1)(Y0 + Y1) over the op's
+        products (7-limb halves; P0 and P2 columns are below the schoolbook columns)."""
+        cols = [0] * 13
+        for x, y, m in op.prods:
+            bx, by = limb_bounds(m * len(x) * P), limb_bounds(len(y) * P)
+            sx = [bx[i] + bx[i + 7] for i in range(7)]
+            sy = [by[j] + by[j + 7] for j in range(7)]
+            for i in range(7):
+                for j in range(7):
+                    cols[i + j] += sx[i] * sy[j]
+        return max(cols) + (1 << 40)
+
     def round_flags(self, ops):
-        """x15 of a round (some m X >= 2^392: X takes 15 limbs), checked against the column bound."""
+        """(x15, kara) of a round, checked against the column bounds: x15 when some m X >= 2^392 (X takes
+        15 limbs, schoolbook products); otherwise one Karatsuba level when its middle columns fit."""
         x15 = int(any(m * len(x) * P >= 1 << 392 for o in ops for x, _, m in o.prods))
         assert all(self.col_bound(o, x15) < 1 << 64 for o in ops), f"{self.name}: a column exceeds 2^64"
-        return x15
+        kara = int(not x15 and KARATSUBA and all(self.kara_bound(o) < 1 << 64 for o in ops))
+        return x15, kara
 
     # ------------------------------------------------------------ encoding
     def encode(self):
         """hdr: 4 u32 per round (wave-uniform):
              w0 = K | nadd << 4 | mflag << 6 | x2 << 7 | y2 << 8 | neg << 9 | inv << 10 | load << 11 |
-                  emit << 12 | shadow << 13 | red << 16 | x15 << 21 | used << 24  (x15: some m X >= 2^392)
+                  emit << 12 | shadow << 13 | red << 16 | x15 << 21 | kara << 22 | used << 24
+                  (x15: some m X >= 2^392; kara: one Karatsuba level in the products)
              w1 = record offset (u32 words), w2 = record words per lane, w3 = 0
            rec: per lane (T lanes per round; lanes >= used: dst = SLOT_NONE):
              r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;
@@ -330,7 +348,7 @@ class Program:
             assert K <= MAXK
             nadd = max(len(o.adds) for o in ops)
             mflag = any(abs(m) != 1 for o in ops for _, _, m in o.prods)
-            x15 = self.round_flags(ops)
+            x15, kara = self.round_flags(ops)
             x2 = any(len(x) == 2 for o in ops for x, _, _ in o.prods)
             y2 = any(len(y) == 2 for o in ops for _, y, _ in o.prods)
             neg = any(t.neg for o in ops for x, y, _ in o.prods for t in x + y)
@@ -344,7 +362,7 @@ class Program:
             words = 4 + 3 * K
             hdr += [K | nadd << 4 | int(mflag) << 6 | int(x2) << 7 | int(y2) << 8 | int(neg) << 9 | int(inv) << 10 |
                     int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | red << 16 |
-                    x15 << 21 | len(ops) << 24,
+                    x15 << 21 | kara << 22 | len(ops) << 24,
                     len(rec), words, 0]
             for lane in range(self.team):
                 w = [0] * words

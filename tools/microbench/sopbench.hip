@@ -27,15 +27,17 @@ __global__ __launch_bounds__(64) void k_op(const uint32_t* rec, uint32_t h0, uin
   out[blockIdx.x * 64 + threadIdx.x] = wr[0];
 }
 
-struct Shape { const char* name; int K, x2, y2, neg, mflag, x15, red, sh; };
+struct Shape { const char* name; int K, x2, y2, neg, mflag, x15, red, sh, kara; };
 
 int main() {
-  Shape shapes[] = {{"K0 red0", 0, 0, 0, 0, 0, 0, 0, 0}, {"K1 red0", 1, 0, 0, 0, 0, 0, 0, 0},
-                    {"K1 red3", 1, 0, 0, 0, 0, 0, 3, 0}, {"K1 red0 shadow", 1, 0, 0, 0, 0, 0, 0, 1},
-                    {"K4 red0", 4, 0, 0, 0, 0, 0, 0, 0}, {"K7 red0", 7, 0, 0, 0, 0, 0, 0, 0},
-                    {"K4 +x2y2 red0", 4, 1, 1, 0, 0, 0, 0, 0}, {"K4 +m red0", 4, 0, 0, 0, 1, 0, 0, 0},
-                    {"K4 +m x15 red0", 4, 0, 0, 0, 1, 1, 0, 0}, {"K3 fexp-like", 3, 1, 0, 0, 1, 0, 3, 1},
-                    {"K7 acc-like", 7, 1, 0, 0, 1, 0, 2, 0}};
+  Shape shapes[] = {{"K0 red0", 0, 0, 0, 0, 0, 0, 0, 0, 0}, {"K1 red0", 1, 0, 0, 0, 0, 0, 0, 0, 0},
+                    {"K1 red0 kara", 1, 0, 0, 0, 0, 0, 0, 0, 1}, {"K1 red3", 1, 0, 0, 0, 0, 0, 3, 0, 0},
+                    {"K4 red0", 4, 0, 0, 0, 0, 0, 0, 0, 0}, {"K4 red0 kara", 4, 0, 0, 0, 0, 0, 0, 0, 1},
+                    {"K7 red0", 7, 0, 0, 0, 0, 0, 0, 0, 0}, {"K7 red0 kara", 7, 0, 0, 0, 0, 0, 0, 0, 1},
+                    {"K4 +x2y2 red0", 4, 1, 1, 0, 0, 0, 0, 0, 0}, {"K4 +m red0", 4, 0, 0, 0, 1, 0, 0, 0, 0},
+                    {"K4 +m x15 red0", 4, 0, 0, 0, 1, 1, 0, 0, 0}, {"K3 fexp-like", 3, 1, 0, 0, 1, 0, 3, 1, 0},
+                    {"K3 fexp-like kara", 3, 1, 0, 0, 1, 0, 3, 1, 1}, {"K7 acc-like", 7, 1, 0, 0, 1, 0, 2, 0, 0},
+                    {"K7 acc-like kara", 7, 1, 0, 0, 1, 0, 2, 0, 1}};
   uint32_t *drec, *dout;
   hipMalloc(&drec, 8 * 64 * 4);
   hipMalloc(&dout, 4096 * 64 * 4);
@@ -59,7 +61,7 @@ int main() {
       }
     }
     const uint32_t h0 = sh.K | (sh.K ? 0u : 1u) << 4 | sh.mflag << 6 | sh.x2 << 7 | sh.y2 << 8 | sh.neg << 9 |
-                        sh.sh << 13 | (uint32_t)sh.red << 16 | sh.x15 << 21 | 1u << 24;
+                        sh.sh << 13 | (uint32_t)sh.red << 16 | sh.x15 << 21 | sh.kara << 22 | 1u << 24;
     hipMemcpy(drec, rec, sizeof(rec), hipMemcpyHostToDevice);
     for (int mode = 0; mode < 2; ++mode) {
       const int blocks = mode ? 2048 : 1;
