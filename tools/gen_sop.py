@@ -308,16 +308,17 @@ class Program:
 
     @staticmethod
     def kara_bound(op):
-        """Largest column of the Karatsuba middle product M = sum_k (X0 + X1)(Y0 + Y1) over the op's
-        products (7-limb halves; P0 and P2 columns are below the schoolbook columns)."""
+        """Largest |column| of the subtractive Karatsuba middle product D = sum_k (X0 - X1)(Y1 - Y0)
+        over the op's products (7-limb halves, signed 64-bit columns on the device; the P0 and P2
+        columns are below the schoolbook columns)."""
         cols = [0] * 13
         for x, y, m in op.prods:
             bx, by = limb_bounds(m * len(x) * P), limb_bounds(len(y) * P)
-            sx = [bx[i] + bx[i + 7] for i in range(7)]
-            sy = [by[j] + by[j + 7] for j in range(7)]
+            dx = [max(bx[i], bx[i + 7]) for i in range(7)]
+            dy = [max(by[j], by[j + 7]) for j in range(7)]
             for i in range(7):
                 for j in range(7):
-                    cols[i + j] += sx[i] * sy[j]
+                    cols[i + j] += dx[i] * dy[j]
         return max(cols) + (1 << 40)
 
     def round_flags(self, ops):
@@ -325,7 +326,7 @@ class Program:
         15 limbs, schoolbook products); otherwise one Karatsuba level when its middle columns fit."""
         x15 = int(any(m * len(x) * P >= 1 << 392 for o in ops for x, _, m in o.prods))
         assert all(self.col_bound(o, x15) < 1 << 64 for o in ops), f"{self.name}: a column exceeds 2^64"
-        kara = int(not x15 and KARATSUBA and all(self.kara_bound(o) < 1 << 64 for o in ops))
+        kara = int(not x15 and KARATSUBA and all(self.kara_bound(o) < 1 << 63 for o in ops))
         return x15, kara
 
     # ------------------------------------------------------------ encoding
