@@ -89,7 +89,7 @@ struct F_sop_lines {
 
 struct F_sop_acc {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -115,7 +115,7 @@ struct F_sop_acc {
 
 struct F_sop_fexp {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -156,7 +156,7 @@ struct F_sop_fexp {
 // formulas), affine H(m) -> W.qh and its identity flag -> W.qh_inf
 struct F_sop_h2c {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + 1,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
