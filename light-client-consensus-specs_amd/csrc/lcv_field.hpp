@@ -9,6 +9,7 @@
 #pragma once
 #include "lcv_common.hpp"
 #include "lcv_consts.inc"
+#include "lcv_col28.hpp"
 
 namespace lcv {
 
@@ -189,8 +190,28 @@ LCV_FN void fp_sqr_ps(uint32_t r[12], const uint32_t a[12]) {
   t[11] = (uint32_t)acc;
   fp_reduce_once(r, t);
 }
+// Round 3: the same Montgomery product / square through the 28-bit column engine (lcv_col28.hpp): no
+// carry chain, one subtractive Karatsuba level, independent columns for a lone wave's issue
+#ifndef LCV_FP_C28
+#define LCV_FP_C28 1
+#endif
+#if LCV_FP_C28
+LCV_FN void fp_mul_c28r(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+  uint32_t t[13];
+  fp_mul_c28(t, a, b);
+  fp_reduce_once(r, t);
+}
+LCV_FN void fp_sqr_c28r(uint32_t r[12], const uint32_t a[12]) {
+  uint32_t t[13];
+  fp_sqr_c28(t, a);
+  fp_reduce_once(r, t);
+}
+#define LCV_SQR_IMPL fp_sqr_c28r
+#define LCV_MUL_IMPL fp_mul_c28r
+#else
 #define LCV_SQR_IMPL fp_sqr_ps
 #define LCV_MUL_IMPL fp_mul_ps
+#endif
 
 // ---- The wide engine (latency mode): ONE item per wave, its values replicated in every lane, and each
 // Montgomery product spread over the lanes — lane c accumulates column c of the 24-column product (12
