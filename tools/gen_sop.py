@@ -628,6 +628,7 @@ def line_program(team=10):
     X, Y, Z = slots2(p, "tx"), slots2(p, "ty"), slots2(p, "tz")
     B, Cp, J, XY, YZ = (slots2(p) for _ in range(5))
     BmF, BpF = slots2(p), slots2(p)
+    C48 = slots2(p)  # 48 C': carries most of 1728 = 36 * 48, so no scaled operand of the T update needs a 15th limb
     la, lb, lc = slots2(p), slots2(p), slots2(p)
     # the addition step's temporaries reuse the doubling step's (different steps, sequential rounds)
     th, lam, Cc, D, E, F, G = B, Cp, J, XY, YZ, BmF, BpF
@@ -657,10 +658,14 @@ def line_program(team=10):
         ops = [Op(dst_of(BmF[c]), [], [(B[c].slot, 1), (Cp[c].slot, -36)]) for c in range(2)]
         ops += [Op(dst_of(BpF[c]), [], [(B[c].slot, 1), (Cp[c].slot, 36)]) for c in range(2)]
         ops += [Op(dst_of(la[c]), [], [(B[c].slot, 1), (Cp[c].slot, -12)], emit=6 * step + c) for c in range(2)]
+        ops += [Op(dst_of(C48[c]), [], [(Cp[c].slot, 48)]) for c in range(2)]
         p.round(ops)
-        # T: X = 2 XY (B - 3E), Y = (B + 3E)^2 - 1728 C'^2, Z = 8 B YZ
+        # T: X = 2 XY (B - 3E), Y = (B + 3E)^2 - 1728 C'^2, Z = 8 B YZ, with 1728 C'^2 taken as
+        # 36 (48 C0 + 48 C1)(C0 - C1) + 72 (48 C0) C1 u: the scaled operands stay below 2^392 (14 limbs,
+        # Karatsuba), where m = 1728 / 3456 on C' itself needed a 15th limb and schoolbook products
+        ysq = [[([C48[0], C48[1]], [Cp[0], ~Cp[1]], -36)], [([C48[0]], [Cp[1]], -72)]]
         ops = [Op(dst_of(X[c]), fp2_prod(XY, BmF, c, m=2)) for c in range(2)]
-        ops += [Op(dst_of(Y[c]), fp2_sqr(BpF, c) + fp2_sqr(Cp, c, m=-1728)) for c in range(2)]
+        ops += [Op(dst_of(Y[c]), fp2_sqr(BpF, c) + ysq[c]) for c in range(2)]
         ops += [Op(dst_of(Z[c]), fp2_prod(B, YZ, c, m=8)) for c in range(2)]
         ops += [Op(dst_of(lb[c]), [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
         ops += [Op(dst_of(lc[c]), [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
@@ -1211,8 +1216,11 @@ def check_fexp(fp):
 def emit(progs, path):
     lines = ["// GENERATED by tools/gen_sop.py — do not edit.  SOP team programs (see lcv_sop.hpp).",
              "#pragma once", "#include <stdint.h>", ""]
+    schoolbook = 0
     for p in progs:
         hdr, rec = p.encode()
+        # a round with products but without the Karatsuba flag needs the device's schoolbook scans
+        schoolbook |= any((w0 & 15) and not (w0 >> 22) & 1 for w0 in hdr[0::4])
         N = p.name.upper()
         lines.append(f"// {p.stats()}")
         lines.append(f"#define LCV_SOP_{N}_TEAM {p.team}")
@@ -1238,6 +1246,8 @@ def emit(progs, path):
             lines.append("  " + ",".join(f"0x{(mv >> (32 * k)) & 0xffffffff:08x}u" for k in range(12)) + ",")
         lines.append("};")
         lines.append("")
+    lines.append("// 1: some product round of these programs is not Karatsuba-eligible (14 x 14 / 15 x 14 schoolbook)")
+    lines.append(f"#define LCV_SOP_SCHOOLBOOK {int(schoolbook)}")
     open(path, "w").write("\n".join(lines) + "\n")
 
 
