@@ -30,10 +30,15 @@ def test_sop_programs_match_oracle():
     GS.check_fexp(progs[2])
     GS.check_h2c(progs[3])
     text = open(os.path.join(H.PKG, "csrc", "lcv_sop_programs.inc")).read()
+    schoolbook = False
     for p in progs:
         hdr, _ = p.encode()
         assert f"#define LCV_SOP_{p.name.upper()}_ROUNDS {len(hdr) // 4}" in text
         assert f"#define LCV_SOP_{p.name.upper()}_SLOTS {p.nslots}" in text
+        schoolbook |= any((w0 & 15) and not (w0 >> 22) & 1 for w0 in hdr[0::4])
+    # the device compiles the schoolbook scans out when no product round needs them (lcv_sop.hpp)
+    assert f"#define LCV_SOP_SCHOOLBOOK {int(schoolbook)}" in text
+    assert not schoolbook, "every product round is Karatsuba since the line walk's 48 C' operand"
 
 
 def test_opcount_every_stage():
