@@ -249,8 +249,33 @@ class Program:
         raise KeyError(c)
 
     # ------------------------------------------------------------ finalise: slot numbers of constants
+    def fold_doublings(self):
+        """A multiplier 2 as a doubled operand (t + t) in rounds where 2 is the only multiplier besides 1
+        and the doubled side's two-term flag is already on: the round then needs no m-scaling of X (12
+        multiply-adds per product on the device, paid by every product of the round) and no new flag.
+        Bounds are unchanged (len(y) * P = 2P = m P).  Idempotent (no m = 2 remains to fold)."""
+        for ops in self.rounds:
+            prods = [pr for o in ops for pr in o.prods]
+            if not any(m != 1 for _, _, m in prods) or any(m not in (1, 2) for _, _, m in prods):
+                continue
+            x2 = any(len(x) == 2 for x, _, _ in prods)
+            y2 = any(len(y) == 2 for _, y, _ in prods)
+            if not all(m == 1 or (y2 and len(y) == 1) or (x2 and len(x) == 1) for x, y, m in prods):
+                continue
+            for o in ops:
+                new = []
+                for x, y, m in o.prods:
+                    if m == 2:
+                        if y2 and len(y) == 1:
+                            y, m = [y[0], y[0]], 1
+                        else:
+                            x, m = [x[0], x[0]], 1
+                    new.append((x, y, m))
+                o.prods = new
+
     def finalize(self):
         self.apply_shadows()
+        self.fold_doublings()
         if 0 not in self.consts:
             self.consts[0] = len(self.consts)
         self.base_const = self.nslots
