@@ -205,28 +205,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
   const uint32_t R = f.P.rounds, ns = f.P.nslots;
   // round r + 1's header and the lane's first record words are loaded at the top of round r
   // (lcv::sop_pre), so their latency overlaps round r's products instead of opening round r + 1
-  uint32_t h0 = 0;
+  uint32_t h0 = 0, h3 = 0;
   const uint32_t* wn = f.P.rec;
   lcv::SopPre pre{0, 0, 0, 0, 0};
   if (R) {
     h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[0]);
     const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[1]);
     const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[2]);
+    h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[3]);
     wn = f.P.rec + off + lane * words;
     if (active) pre = lcv::sop_pre(h0, wn);
   }
   for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t ch0 = h0;
+    const uint32_t ch0 = h0, ch3 = h3;
     const uint32_t* w = wn;  // this round's record (its address computed once, a round ahead)
     const lcv::SopPre cur = pre;
     if (r + 1 < R) {
       h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 4]);
       const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 5]);
       const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 6]);
+      h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 7]);
       wn = f.P.rec + off + lane * words;
       if (active) pre = lcv::sop_pre(h0, wn);
     }
-    if (active) lcv::sop_exec(ch0, w, cur, my, my, lds, ns, io_in, io_out);
+    if (active) lcv::sop_exec(ch0, ch3, w, cur, my, my, lds, ns, io_in, io_out);
     __syncthreads();
   }
   if (active) f.epilogue(item, lane, my);

@@ -273,9 +273,18 @@ class Program:
                     new.append((x, y, m))
                 o.prods = new
 
+    def order_products(self):
+        """Each lane's products two-term first (the sum is order-free): the round's per-product masks
+        (header w3) then mark fewer product indices, and the device skips the second term's LDS loads
+        and the 12-word add wherever no lane of the round needs one.  Idempotent."""
+        for ops in self.rounds:
+            for o in ops:
+                o.prods = sorted(o.prods, key=lambda t: (-(len(t[0]) + len(t[1])), -len(t[0])))
+
     def finalize(self):
         self.apply_shadows()
         self.fold_doublings()
+        self.order_products()
         if 0 not in self.consts:
             self.consts[0] = len(self.consts)
         self.base_const = self.nslots
@@ -360,7 +369,10 @@ class Program:
              w0 = K | nadd << 4 | mflag << 6 | x2 << 7 | y2 << 8 | neg << 9 | inv << 10 | load << 11 |
                   emit << 12 | shadow << 13 | red << 16 | x15 << 21 | kara << 22 | used << 24
                   (x15: some m X >= 2^392; kara: one Karatsuba level in the products)
-             w1 = record offset (u32 words), w2 = record words per lane, w3 = 0
+             w1 = record offset (u32 words), w2 = record words per lane,
+             w3 = xmask | ymask << 16: bit k set when some lane's product k has a two-term X (Y); each
+                  lane's products are ordered two-term first (Program.order_products), so the device
+                  loads and adds a second term only for the product indices that need one
            rec: per lane (T lanes per round; lanes >= used: dst = SLOT_NONE):
              r0 = dst | flags << 12 (1 inv, 2 load, 4 emit) | ld_slot << 16;
              r1 = io index | dst_shadow << 12 | load_shadow << 22  (shadow slots 10 bits, 0x3FF = none);
@@ -385,11 +397,16 @@ class Program:
             shadow = any(o.dst_shadow is not None or o.load_shadow is not None for o in ops)
             red = max(self.red_steps(o) for o in ops)
             assert red <= 10, "result above 2^392"
+            xmask = ymask = 0
+            for o in ops:
+                for k, (x, y, _) in enumerate(o.prods):
+                    xmask |= (len(x) == 2) << k
+                    ymask |= (len(y) == 2) << k
             words = 4 + 3 * K
             hdr += [K | nadd << 4 | int(mflag) << 6 | int(x2) << 7 | int(y2) << 8 | int(neg) << 9 | int(inv) << 10 |
                     int(load) << 11 | int(emit) << 12 | int(shadow) << 13 | red << 16 |
                     x15 << 21 | kara << 22 | len(ops) << 24,
-                    len(rec), words, 0]
+                    len(rec), words, xmask | ymask << 16]
             for lane in range(self.team):
                 w = [0] * words
                 if lane >= len(ops):
@@ -439,7 +456,7 @@ class Program:
             mem[self.base_const + k] = mont(v)
         z = self.zero
         for r in range(len(hdr) // 4):
-            w0, off, words = hdr[4 * r], hdr[4 * r + 1], hdr[4 * r + 2]
+            w0, off, words, w3 = hdr[4 * r], hdr[4 * r + 1], hdr[4 * r + 2], hdr[4 * r + 3]
             K, nadd, mflag, red, used = w0 & 15, (w0 >> 4) & 3, (w0 >> 6) & 1, (w0 >> 16) & 31, w0 >> 24
             writes = []
             for lane in range(self.team):
@@ -457,8 +474,11 @@ class Program:
                 acc = 0
                 for k in range(K):
                     a, b, m = w[4 + 3 * k:7 + 3 * k]
-                    X = term(a & 0xFFFF) + term(a >> 16)
-                    Y = term(b & 0xFFFF) + term(b >> 16)
+                    tx, ty = (w3 >> k) & 1, (w3 >> (16 + k)) & 1   # second term loaded at all?
+                    assert tx or a >> 16 == z, "a two-term X outside the round's x mask"
+                    assert ty or b >> 16 == z, "a two-term Y outside the round's y mask"
+                    X = term(a & 0xFFFF) + (term(a >> 16) if tx else 0)
+                    Y = term(b & 0xFFFF) + (term(b >> 16) if ty else 0)
                     if mflag:
                         X *= m
                     else:

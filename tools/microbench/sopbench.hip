@@ -23,7 +23,7 @@ __global__ __launch_bounds__(64) void k_op(const uint32_t* rec, uint32_t h0, uin
   if (threadIdx.x == 0)
     for (int j = 0; j < 24; ++j) cl[j] = 0;
   __syncthreads();
-  for (int it = 0; it < ITER; ++it) lcv::sop_exec(h0, rec + (threadIdx.x & 7) * words, lcv::sop_pre(h0, rec + (threadIdx.x & 7) * words), in, wr, cl, NS, nullptr, nullptr);
+  for (int it = 0; it < ITER; ++it) lcv::sop_exec(h0, ((h0 >> 7) & 1u ? 0xFFFFu : 0u) | ((h0 >> 8) & 1u ? 0xFFFF0000u : 0u), rec + (threadIdx.x & 7) * words, lcv::sop_pre(h0, rec + (threadIdx.x & 7) * words), in, wr, cl, NS, nullptr, nullptr);
   out[blockIdx.x * 64 + threadIdx.x] = wr[0];
 }
 

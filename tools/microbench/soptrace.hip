@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_
     const uint32_t h0 = __builtin_amdgcn_readfirstlane(P.hdr[4 * r]);
     const uint32_t off = __builtin_amdgcn_readfirstlane(P.hdr[4 * r + 1]);
     const uint32_t words = __builtin_amdgcn_readfirstlane(P.hdr[4 * r + 2]);
-    if (active) lcv::sop_exec(h0, P.rec + off + lane * words, lcv::sop_pre(h0, P.rec + off + lane * words), my, my, lds, P.nslots, io_item, io_item);
+    if (active) lcv::sop_exec(h0, __builtin_amdgcn_readfirstlane(P.hdr[4 * r + 3]), P.rec + off + lane * words, lcv::sop_pre(h0, P.rec + off + lane * words), my, my, lds, P.nslots, io_item, io_item);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
