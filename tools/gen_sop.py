@@ -49,6 +49,7 @@ KARATSUBA = True                   # device products: one Karatsuba level where 
 MAXK = 15
 SLOT_MASK = 0xFFF
 NEG = 0x8000                       # term halfword: slot | NEG
+PCONST = 0x8000                    # product-term halfword: 48 * slot, or PCONST | 48 * constant index
 SHADOW_NONE = 0x3FF                # record word 1: no shadow slot
 
 
@@ -291,6 +292,15 @@ class Program:
         self.zero = self.base_const + self.consts[0]
         assert self.base_const + len(self.consts) < SLOT_MASK
 
+    def pterm(self, s):
+        """Product-term halfword of slot or constant s: PCONST (constant) | the value's byte offset in its
+        LDS table; the device address is lds + offset + (flag ? constants - lds : 0) (lcv_sop.hpp
+        sop_pterm: four instructions, no compare)."""
+        s = self.sl(s)
+        h = PCONST | 48 * (s - self.base_const) if s >= self.base_const else 48 * s
+        assert 48 * max(self.nslots, len(self.consts)) < PCONST
+        return h
+
     def sl(self, s):
         if isinstance(s, tuple):
             return self.base_const + s[1]
@@ -381,6 +391,7 @@ class Program:
         self.finalize()
         hdr, rec = [], []
         z = self.zero
+        zp = self.pterm(z)
         for ops in self.rounds:
             K = max(len(o.prods) for o in ops)
             assert K <= MAXK
@@ -413,7 +424,7 @@ class Program:
                     w[0] = SLOT_MASK
                     w[2] = w[3] = z
                     for k in range(K):
-                        w[4 + 3 * k:7 + 3 * k] = [z | z << 16, z | z << 16, 1]
+                        w[4 + 3 * k:7 + 3 * k] = [zp | zp << 16, zp | zp << 16, 1]
                     rec += w
                     continue
                 o = ops[lane]
@@ -438,12 +449,12 @@ class Program:
                         x, y, m = o.prods[k]
                         if m < 0:
                             x, m = [~t for t in x], -m
-                        th = lambda t: self.sl(t.slot) | (NEG if t.neg else 0)  # noqa: E731
-                        xs = [th(t) for t in x] + [z] * (2 - len(x))
-                        ys = [th(t) for t in y] + [z] * (2 - len(y))
+                        assert not any(t.neg for t in x + y)
+                        xs = [self.pterm(t.slot) for t in x] + [zp] * (2 - len(x))
+                        ys = [self.pterm(t.slot) for t in y] + [zp] * (2 - len(y))
                         w[4 + 3 * k:7 + 3 * k] = [xs[0] | xs[1] << 16, ys[0] | ys[1] << 16, m]
                     else:
-                        w[4 + 3 * k:7 + 3 * k] = [z | z << 16, z | z << 16, 1]
+                        w[4 + 3 * k:7 + 3 * k] = [zp | zp << 16, zp | zp << 16, 1]
                 rec += w
         return hdr, rec
 
@@ -467,16 +478,17 @@ class Program:
                     continue
 
                 def term(h):
-                    s = h & SLOT_MASK
+                    s = (self.base_const if h & PCONST else 0) + (h & (PCONST - 1)) // 48
                     v = mem[s]
                     assert 0 <= v <= P   # a shadow slot holds p - v in (0, p]
-                    return (P - v) if h & NEG else v
+                    return v
                 acc = 0
                 for k in range(K):
                     a, b, m = w[4 + 3 * k:7 + 3 * k]
                     tx, ty = (w3 >> k) & 1, (w3 >> (16 + k)) & 1   # second term loaded at all?
-                    assert tx or a >> 16 == z, "a two-term X outside the round's x mask"
-                    assert ty or b >> 16 == z, "a two-term Y outside the round's y mask"
+                    zp = self.pterm(z)
+                    assert tx or a >> 16 == zp, "a two-term X outside the round's x mask"
+                    assert ty or b >> 16 == zp, "a two-term Y outside the round's y mask"
                     X = term(a & 0xFFFF) + (term(a >> 16) if tx else 0)
                     Y = term(b & 0xFFFF) + (term(b >> 16) if ty else 0)
                     if mflag:
