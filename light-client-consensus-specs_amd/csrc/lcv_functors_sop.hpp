@@ -11,15 +11,19 @@
 #include "lcv_sop_programs.inc"
 
 enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
+// per-item LDS pitch = 12 * slots + SOP_PITCH_PAD words: 4 keeps every value 16-byte aligned for the
+// b128 LDS accesses (LCV_SOP_B128, lcv_sop.hpp); 1 (odd) staggers the teams' banks for 32-bit accesses
+enum { SOP_PITCH_PAD = LCV_SOP_B128 ? 4 : 1 };
 
-// Every SOP functor pads its per-item LDS pitch to an odd word count: the teams of a wave then start
-// on different LDS banks (tools: a bank model of the programs gives 1.3-1.4x the conflict-free LDS
-// cycles instead of 2.7-3.4x with the 12 * slots pitch, which is a multiple of 32 words or 16 off one)
+// Round 2 padded the pitch to an odd word count so the teams of a wave start on different LDS banks for
+// 32-bit accesses (a bank model: 1.3-1.4x the conflict-free LDS cycles instead of 2.7-3.4x); since r03
+// v13 the pitch is 4 mod 8 words and values move as 16-byte accesses, three instead of six LDS
+// instructions per value: 1.448 -> 1.472 M updates/s in a same-box A/B (profiles/r03_v13)
 struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + 1,
+  static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
   LCV_HD uint32_t upd(uint32_t t) const { return mode == 0 ? t >> 1 : t; }
@@ -90,7 +94,7 @@ struct F_sop_lines {
 struct F_sop_acc {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + 1,
+  static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
   LCV_HD const uint32_t* io_in(uint32_t i) const { return W.lines + (size_t)i * SOP_LINE_WORDS; }
@@ -116,7 +120,7 @@ struct F_sop_acc {
 struct F_sop_fexp {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + 1,
+  static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
   static_assert(LCV_SOP_FEXP_SLOT_R5_1 == LCV_SOP_FEXP_SLOT_R0_0 + 11, "r in consecutive slots");
@@ -157,7 +161,7 @@ struct F_sop_fexp {
 struct F_sop_h2c {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
-  static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + 1,
+  static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
   static_assert(LCV_SOP_H2C_SLOT_HY1 == LCV_SOP_H2C_SLOT_HX0 + 3, "hx, hy in consecutive slots");
@@ -192,7 +196,7 @@ template <class F>
 // a smaller LDS than gfx950's 160 KB and gives the kernel 256 VGPRs (2 waves/SIMD).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) void k_sop(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
-  extern __shared__ uint32_t lds[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // 16-byte aligned values (LCV_SOP_B128)
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
   const uint32_t item = blockIdx.x * G + team;
   const bool active = team < G && item < n;
