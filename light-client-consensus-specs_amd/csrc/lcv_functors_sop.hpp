@@ -119,7 +119,7 @@ struct F_sop_acc {
 
 struct F_sop_fexp {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
