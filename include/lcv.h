@@ -173,6 +173,16 @@ int lcv_validate_sharded(lcv_ctx* ctx, lcv_dbatch* b, uint64_t current_slot, con
                          uint64_t per_rank, uint8_t* verdict_all_out);
 /* max over ranks of one double (in place); doubles as a barrier */
 int lcv_comm_allreduce_max(lcv_ctx* ctx, double* inout);
+/* Failure containment (a failed GPU's shard is re-run).  Every collective completes within
+ * the communicator timeout (default 60 s) or the call fails with LCV_EDEVICE: the wait polls the stream and
+ * RCCL's asynchronous error (ncclCommGetAsyncError), so a rank whose peer died or hangs returns instead of
+ * blocking in ncclAllGather.  The communicator is then marked failed (collectives refused, LCV_ESTATE) until
+ * the surviving ranks all call lcv_comm_shrink with the same list of excluded ranks (ncclCommShrink with
+ * NCCL_SHRINK_ABORT: the failed parent's operations are terminated, the survivors renumbered in rank
+ * order; new_rank / new_nranks out), or lcv_comm_abort (ncclCommAbort) drops it. */
+int lcv_comm_set_timeout(lcv_ctx* ctx, double seconds);
+int lcv_comm_shrink(lcv_ctx* ctx, const int* exclude_ranks, int nexclude, int* new_rank, int* new_nranks);
+int lcv_comm_abort(lcv_ctx* ctx);
 
 /* ---- bls.FastAggregateVerify (sync-protocol.md:464); py_ecc semantics (every key KeyValidated).
  * Any number of pubkeys (npk = 0 -> False), a message of any length (the light-client call site passes

@@ -7,7 +7,9 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <chrono>
 #include <new>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -70,6 +72,9 @@ static void be_comm_destroy(lcv_ctx* ctx);
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank);
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout);
 static int be_comm_count(lcv_ctx* ctx, int* out);
+static int be_comm_wait(lcv_ctx* ctx);
+static int be_comm_shrink(lcv_ctx* ctx, const int* exclude, int nexclude, int* rank, int* nranks);
+static void be_comm_abort(lcv_ctx* ctx);
 static int be_host_alloc(lcv_ctx* ctx, void** p, size_t bytes);
 static void be_host_free(lcv_ctx* ctx, void* p);
 static int be_wait_event(lcv_ctx* ctx, int ev);
@@ -328,6 +333,51 @@ static int be_comm_count(lcv_ctx* ctx, int* out) {
   *out = c;
   return LCV_OK;
 }
+// Waits for the current stream (a collective and what follows it) with a bound: polls the stream and
+// RCCL's asynchronous error; a peer that died or hangs fails the call (LCV_EDEVICE, the context's
+// communicator marked failed) instead of blocking this rank forever in the collective.
+static int be_comm_wait_stream(lcv_ctx* ctx, hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned it = 0;; ++it) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return LCV_OK;
+    if (q != hipErrorNotReady) {
+      ctx->comm_failed = true;
+      return fail(ctx, LCV_EDEVICE, std::string("collective: ") + hipGetErrorString(q));
+    }
+    ncclResult_t ae = ncclSuccess;
+    if (ncclCommGetAsyncError(ctx->be.comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+      ctx->comm_failed = true;
+      return fail(ctx, LCV_EDEVICE, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > ctx->comm_timeout_s) {
+      ctx->comm_failed = true;
+      return fail(ctx, LCV_EDEVICE, "collective did not complete within the communicator timeout (a peer rank died or hangs)");
+    }
+    if (it >= 256) std::this_thread::sleep_for(std::chrono::microseconds(50));  // spin briefly first
+  }
+}
+static int be_comm_wait(lcv_ctx* ctx) { return be_comm_wait_stream(ctx, cur_stream(ctx)); }
+// the survivors' communicator: ncclCommShrink terminates the failed parent's operations (a collective
+// stuck on a dead peer) and builds the new one; the parent is then aborted
+static int be_comm_shrink(lcv_ctx* ctx, const int* exclude, int nexclude, int* rank, int* nranks) {
+  HIPCHK(ctx, hipSetDevice(ctx->be.device));
+  ncclComm_t nc = nullptr;
+  ncclResult_t r = ncclCommShrink(ctx->be.comm, const_cast<int*>(exclude), nexclude, &nc, nullptr, NCCL_SHRINK_ABORT);
+  if (r != ncclSuccess || !nc) return nccl_fail(ctx, r, "ncclCommShrink");
+  (void)ncclCommAbort(ctx->be.comm);
+  ctx->be.comm = nc;
+  if ((r = ncclCommUserRank(nc, rank)) != ncclSuccess) return nccl_fail(ctx, r, "ncclCommUserRank");
+  if ((r = ncclCommCount(nc, nranks)) != ncclSuccess) return nccl_fail(ctx, r, "ncclCommCount");
+  return be_sync(ctx);  // the aborted collective no longer holds the streams
+}
+static void be_comm_abort(lcv_ctx* ctx) {
+  (void)hipSetDevice(ctx->be.device);
+  if (ctx->be.comm) (void)ncclCommAbort(ctx->be.comm);
+  if (ctx->be.comm_scalar) (void)hipFree(ctx->be.comm_scalar);
+  ctx->be.comm = nullptr;
+  ctx->be.comm_scalar = nullptr;
+}
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
   hipStream_t s = ctx->be.st[0];
@@ -335,8 +385,7 @@ static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   ncclResult_t r = ncclAllReduce(ctx->be.comm_scalar, ctx->be.comm_scalar, 1, ncclFloat64, ncclMax, ctx->be.comm, s);
   if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllReduce");
   HIPCHK(ctx, hipMemcpyAsync(inout, ctx->be.comm_scalar, sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(ctx, hipStreamSynchronize(s));
-  return LCV_OK;
+  return be_comm_wait_stream(ctx, s);
 }
 
 extern "C" int lcv_device_count(int* out) {

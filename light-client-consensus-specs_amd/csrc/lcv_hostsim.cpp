@@ -8,6 +8,8 @@
 #include <fstream>
 #include <new>
 #include <thread>
+#include <errno.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <stdlib.h>
 #include <string>
@@ -71,6 +73,9 @@ static void be_comm_destroy(lcv_ctx* ctx);
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank);
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout);
 static int be_comm_count(lcv_ctx* ctx, int* out);
+static int be_comm_wait(lcv_ctx* ctx);
+static int be_comm_shrink(lcv_ctx* ctx, const int* exclude, int nexclude, int* rank, int* nranks);
+static void be_comm_abort(lcv_ctx* ctx);
 static int be_host_alloc(lcv_ctx* ctx, void** p, size_t bytes);
 static void be_host_free(lcv_ctx*, void* p) { free(p); }
 static int be_wait_event(lcv_ctx*, int) { return 0; }
@@ -193,7 +198,10 @@ static int comm_exchange(lcv_ctx* ctx, const void* mine, size_t bytes, uint8_t* 
         f.read((char*)all + (size_t)k * bytes, (std::streamsize)bytes);
         if ((size_t)f.gcount() == bytes) break;
       }
-      if (t > 120000) return fail(ctx, LCV_EDEVICE, "hostsim comm: timed out waiting for a rank");
+      if (t > 1000.0 * ctx->comm_timeout_s) {
+        ctx->comm_failed = true;
+        return fail(ctx, LCV_EDEVICE, "hostsim comm: collective did not complete within the communicator timeout");
+      }
       std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
   }
@@ -206,6 +214,32 @@ static int be_comm_count(lcv_ctx* ctx, int* out) {
   *out = ctx->be.comm_n;
   return LCV_OK;
 }
+static int be_comm_wait(lcv_ctx*) { return LCV_OK; }  // the stand-in's exchanges are synchronous
+// the survivors renumber in rank order and continue in a sub-directory every survivor names alike
+static int be_comm_shrink(lcv_ctx* ctx, const int* exclude, int nexclude, int* rank, int* nranks) {
+  Backend& b = ctx->be;
+  std::vector<bool> gone((size_t)b.comm_n, false);
+  for (int i = 0; i < nexclude; ++i) gone[(size_t)exclude[i]] = true;
+  std::string sub = b.comm_dir + "/shrink";
+  int r = 0, n = 0;
+  for (int k = 0; k < b.comm_n; ++k) {
+    if (gone[(size_t)k]) {
+      sub += "_" + std::to_string(k);
+      continue;
+    }
+    if (k == b.comm_rank) r = n;
+    ++n;
+  }
+  if (mkdir(sub.c_str(), 0700) != 0 && errno != EEXIST) return fail(ctx, LCV_EDEVICE, "hostsim comm: shrink directory");
+  b.comm_dir = sub;
+  b.comm_rank = r;
+  b.comm_n = n;
+  b.comm_round = 0;
+  *rank = r;
+  *nranks = n;
+  return LCV_OK;
+}
+static void be_comm_abort(lcv_ctx* ctx) { ctx->be.comm_dir.clear(); }
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   std::vector<double> all((size_t)ctx->be.comm_n);
   LCV_TRY(comm_exchange(ctx, inout, sizeof(double), (uint8_t*)all.data()));

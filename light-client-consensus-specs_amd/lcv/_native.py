@@ -78,6 +78,9 @@ SIGNATURES = {
     "lcv_comm_destroy": (C.c_int, [C.c_void_p]),
     "lcv_validate_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u8p, C.c_uint64, u8p]),
     "lcv_comm_allreduce_max": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    "lcv_comm_set_timeout": (C.c_int, [C.c_void_p, C.c_double]),
+    "lcv_comm_shrink": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "lcv_comm_abort": (C.c_int, [C.c_void_p]),
     "lcv_fast_aggregate_verify": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u8p, C.c_uint64, u8p, C.POINTER(C.c_int)]),
     "lcv_fast_aggregate_verify_batch": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u32p, u8p, u8p, u8p, C.c_uint64, u8p]),
     "lcv_merkle_branch_batch": (C.c_int, [C.c_void_p, u8p, u8p, C.c_uint32, C.c_uint64, u8p, C.c_uint64, u8p]),

@@ -112,6 +112,7 @@ class Verifier:
             raise LcvError(f"lcv_init(device={device}) failed with status {rc}")
         self.device = device
         self.config = _config.MAINNET  # the context's network configuration (lcv_init: mainnet)
+        self.latency_mode = 32  # lcv_set_latency_mode's value (lcv_init's default)
 
     # ------------------------------------------------------------------ plumbing
     def _check(self, rc: int, what: str):
@@ -149,6 +150,7 @@ class Verifier:
         (one item per wave, products spread over the lanes; identical results); 0 = the batch engine
         always (default 32)."""
         self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
+        self.latency_mode = int(max_rows)
 
     def last_timings(self) -> Dict[str, float]:
         ms = (C.c_float * 16)()

@@ -93,14 +93,94 @@ def rendezvous(lib, rank: int, world: int, key: Optional[str] = None, timeout: f
         time.sleep(0.01)
 
 
-class Comm:
-    """The RCCL communicator of one rank (on `verifier`'s device)."""
+class CommFailed(LcvError):
+    """A collective failed or timed out (a peer rank died or hangs); the communicator must be shrunk to
+    the surviving ranks (Comm.recover) before the next collective."""
 
-    def __init__(self, verifier, world: int, rank: int, key: Optional[str] = None):
+
+class Comm:
+    """The RCCL communicator of one rank (on `verifier`'s device).  `timeout`: every collective completes
+    within it or fails with CommFailed (lcv_comm_set_timeout); `recover()` then agrees on the surviving
+    ranks and shrinks the communicator to them (lcv_comm_shrink)."""
+
+    def __init__(self, verifier, world: int, rank: int, key: Optional[str] = None, timeout: float = 60.0):
         self.v, self.world, self.rank = verifier, int(world), int(rank)
         self.key = key
+        self.epoch = 0          # recoveries so far
+        self.ranks = list(range(self.world))  # original rank ids of the current members, by new rank
         uid = rendezvous(verifier.lib, self.rank, self.world, key)
         self.v._check(self.v.lib.lcv_comm_init(self.v.ctx, self.world, self.rank, ptr(as_u8(uid))), "lcv_comm_init")
+        self.set_timeout(timeout)
+
+    def set_timeout(self, seconds: float) -> None:
+        self.v._check(self.v.lib.lcv_comm_set_timeout(self.v.ctx, float(seconds)), "lcv_comm_set_timeout")
+
+    def _coll(self, rc: int, what: str) -> None:
+        """Collective status: LCV_EDEVICE (-2) from a collective = the communicator failed."""
+        if rc == -2:
+            msg = self.v.lib.lcv_last_error(self.v.ctx)
+            raise CommFailed(f"{what}: {msg.decode() if msg else 'collective failed'}")
+        self.v._check(rc, what)
+
+    # ---- failure containment (SURVEY.md §5): membership agreement through the rendezvous directory
+    def _fail_path(self, what: str) -> str:
+        return f"{_id_path(self.key)}.{launch_tag_safe()}.fail{self.epoch}.{what}"
+
+    def agree_survivors(self, grace: float = 10.0) -> list:
+        """After a failed collective: every live member announces itself, waits until all members did or
+        `grace` seconds passed, and the first to publish a decision (exclusive create) fixes the survivor
+        list everyone then uses; a member left out of the decision (it announced too late) raises."""
+        me = self.ranks[self.rank]
+        open(self._fail_path(f"alive.{me}"), "w").close()
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < grace:
+            if all(os.path.exists(self._fail_path(f"alive.{r}")) for r in self.ranks):
+                break
+            if os.path.exists(self._fail_path("decision")):
+                break
+            time.sleep(0.01)
+        alive = [r for r in self.ranks if os.path.exists(self._fail_path(f"alive.{r}"))]
+        dec = self._fail_path("decision")
+        try:
+            fd = os.open(dec + ".tmp." + str(me), os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+            os.write(fd, (",".join(map(str, alive))).encode())
+            os.close(fd)
+            os.link(dec + ".tmp." + str(me), dec)  # atomic exclusive publish: the first link wins
+        except FileExistsError:
+            pass
+        finally:
+            try:
+                os.remove(dec + ".tmp." + str(me))
+            except OSError:
+                pass
+        for _ in range(1000):
+            try:
+                txt = open(dec).read()
+                if txt:
+                    break
+            except FileNotFoundError:
+                pass
+            time.sleep(0.01)
+        survivors = [int(x) for x in txt.split(",")]
+        if me not in survivors:
+            raise CommFailed(f"rank {me} was excluded by the survivors' decision {survivors}")
+        return survivors
+
+    def recover(self, grace: float = 10.0) -> list:
+        """Shrink the failed communicator to the surviving ranks (same decision on every survivor);
+        returns the survivors' original rank ids.  Afterwards self.rank / self.world are the new ones."""
+        survivors = self.agree_survivors(grace)
+        exclude = [k for k, r in enumerate(self.ranks) if r not in survivors]
+        ex = (C.c_int * max(1, len(exclude)))(*exclude)
+        nr, nn = C.c_int(), C.c_int()
+        self.v._check(self.v.lib.lcv_comm_shrink(self.v.ctx, ex, len(exclude), C.byref(nr), C.byref(nn)),
+                      "lcv_comm_shrink")
+        self.ranks = [r for r in self.ranks if r in survivors]
+        self.rank, self.world = int(nr.value), int(nn.value)
+        if self.world != len(self.ranks):
+            raise CommFailed(f"shrunk communicator has {self.world} ranks, the survivors' decision {len(self.ranks)}")
+        self.epoch += 1
+        return survivors
 
     def validate_sharded(self, rb, current_slot: int, genesis_validators_root: bytes, per_rank: int,
                          out: Optional[np.ndarray] = None) -> np.ndarray:
@@ -108,16 +188,16 @@ class Comm:
         bytes: (world * per_rank,) uint8, rank-major, each slice zero padded."""
         gvr = as_u8(bytes(genesis_validators_root))
         buf = out if out is not None else np.zeros(self.world * per_rank, np.uint8)
-        self.v._check(self.v.lib.lcv_validate_sharded(self.v.ctx, rb.handle, int(current_slot), ptr(gvr),
-                                                      int(per_rank), ptr(buf)), "lcv_validate_sharded")
+        self._coll(self.v.lib.lcv_validate_sharded(self.v.ctx, rb.handle, int(current_slot), ptr(gvr),
+                                                   int(per_rank), ptr(buf)), "lcv_validate_sharded")
         return buf
 
     def slot_allgather(self, slot: int, n: int, per_rank: int, out: Optional[np.ndarray] = None) -> np.ndarray:
         """After this rank's batch in work-space slot `slot` (Verifier.validate_resident_async), all-gather
         every rank's verdict bytes: (world * per_rank,) uint8, rank-major, each slice zero padded."""
         buf = out if out is not None else np.zeros(self.world * per_rank, np.uint8)
-        self.v._check(self.v.lib.lcv_slot_allgather(self.v.ctx, int(slot), int(n), int(per_rank), ptr(buf)),
-                      "lcv_slot_allgather")
+        self._coll(self.v.lib.lcv_slot_allgather(self.v.ctx, int(slot), int(n), int(per_rank), ptr(buf)),
+                   "lcv_slot_allgather")
         return buf
 
     def count(self) -> int:
@@ -128,7 +208,7 @@ class Comm:
 
     def allreduce_max(self, x: float) -> float:
         d = C.c_double(float(x))
-        self.v._check(self.v.lib.lcv_comm_allreduce_max(self.v.ctx, C.byref(d)), "lcv_comm_allreduce_max")
+        self._coll(self.v.lib.lcv_comm_allreduce_max(self.v.ctx, C.byref(d)), "lcv_comm_allreduce_max")
         return d.value
 
     def barrier(self) -> None:
@@ -136,12 +216,17 @@ class Comm:
 
     def close(self) -> None:
         if self.v is not None:
-            self.barrier()
+            try:
+                self.barrier()
+            except CommFailed:
+                pass  # a failed communicator is aborted by lcv_comm_destroy
             if self.rank == 0:
-                try:
-                    os.remove(_id_path(self.key))
-                except OSError:
-                    pass
+                import glob
+                for f in [_id_path(self.key)] + glob.glob(f"{_id_path(self.key)}.*.fail*"):
+                    try:
+                        os.remove(f)
+                    except OSError:
+                        pass
             self.v.lib.lcv_comm_destroy(self.v.ctx)
             self.v = None
 
@@ -154,18 +239,36 @@ def unshard(gathered: np.ndarray, n_total: int, world: int) -> np.ndarray:
     return np.concatenate(parts) if parts else gathered[:0]
 
 
-def validate_sharded(verifier, batch, current_slot: int, genesis_validators_root: bytes, comm: Comm) -> np.ndarray:
+def validate_sharded(verifier, batch, current_slot: int, genesis_validators_root: bytes, comm: Comm,
+                     recover: bool = True, grace: float = 10.0) -> np.ndarray:
     """This rank validates its shard of `batch` (the full PackedUpdates, identical on every rank);
-    returns the full verdict array (bool) on every rank.  The store must already be set on `verifier`."""
-    world, rank = comm.world, comm.rank
-    lo, hi = shard_bounds(batch.n, world, rank)
-    per = -(-batch.n // world)
-    if hi > lo:
-        rb = verifier.upload(batch.slice(lo, hi))
-    else:  # an empty shard still joins the collective (a one-row dummy batch, verdict overwritten)
-        rb = verifier.upload(batch.slice(0, 1))
-    try:
-        g = comm.validate_sharded(rb, current_slot, genesis_validators_root, max(per, 1))
-    finally:
-        rb.free()
-    return unshard(g, batch.n, world).astype(bool)
+    returns the full verdict array (bool) on every rank.  The store must already be set on `verifier`.
+
+    Failure containment: when a peer dies or hangs, the collective fails within the
+    communicator's timeout on every surviving rank (CommFailed); with `recover` the survivors agree on
+    who is left (Comm.recover), shrink the communicator to themselves and the batch is re-sharded over
+    them — the failed rank's shard is validated on the survivors — until a pass completes.  The result
+    equals the single-rank verdicts."""
+    while True:
+        world, rank = comm.world, comm.rank
+        lo, hi = shard_bounds(batch.n, world, rank)
+        per = -(-batch.n // world)
+        if os.environ.get("LCV_TEST_FAIL_RANK") == str(comm.ranks[rank]) and comm.epoch == 0:
+            os._exit(17)  # test hook (tests/test_multi.py): this rank dies before its collective
+        if hi > lo:
+            rb = verifier.upload(batch.slice(lo, hi))
+        else:  # an empty shard still joins the collective (a one-row dummy batch, verdict overwritten)
+            rb = verifier.upload(batch.slice(0, 1))
+        try:
+            g = comm.validate_sharded(rb, current_slot, genesis_validators_root, max(per, 1))
+            return unshard(g, batch.n, world).astype(bool)
+        except CommFailed:
+            if not recover or world == 1:
+                raise
+            comm.recover(grace)
+        finally:
+            rb.free()
+
+
+def launch_tag_safe() -> str:
+    return "".join(c if c.isalnum() or c in "._-" else "_" for c in launch_tag())

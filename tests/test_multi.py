@@ -83,3 +83,45 @@ def test_two_rank_gloo():
     for rank, full, gloo, exp, t, slots in res:
         assert full == exp == gloo == slots[0] == slots[1]
         assert t == 2.0
+
+
+def _fail_worker(rank, world, dead, port, q):
+    """Rank `dead` dies before its collective (lcv.multi's LCV_TEST_FAIL_RANK hook); the survivors'
+    collective times out (communicator timeout 3 s), they agree on who is left, shrink the communicator
+    and re-validate the batch over themselves."""
+    os.environ["LCV_TEST_FAIL_RANK"] = str(dead)
+    from lcv import multi, synth
+    v = H.hostsim_verifier()
+    kinds = np.array([0, 2, 4, 1, 5, 0, 6, 3, 0, 1, 0])
+    sb = synth.generate(v, len(kinds), seed=33, kinds=kinds)
+    v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    comm = multi.Comm(v, world, rank, key=f"fail_{port}", timeout=3.0)
+    full = multi.validate_sharded(v, sb.updates, sb.current_slot, sb.genesis_validators_root, comm, grace=3.0)
+    single, _ = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    t = comm.allreduce_max(float(rank + 1))  # the shrunk communicator keeps working
+    q.put((rank, full.tolist(), single.astype(bool).tolist(), sb.expected_verdict.tolist(), comm.world, comm.ranks, t))
+    comm.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,dead", [(2, 1), (4, 2)])
+def test_rank_failure_recovery(world, dead):
+    """SURVEY.md §5 (a GPU failing in a shard -> rerun the shard): with one rank dead mid-batch the
+    survivors return, and their verdicts equal the single-rank result."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, dead, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=500) for _ in range(world - 1)]
+    for r, p in enumerate(procs):
+        p.join(120)
+        assert p.exitcode == (17 if r == dead else 0), (r, p.exitcode)
+    survivors = [r for r in range(world) if r != dead]
+    assert sorted(x[0] for x in res) == survivors
+    for rank, full, single, exp, w, ranks, t in res:
+        assert full == single == exp
+        assert w == world - 1 and ranks == survivors
+        assert t == float(max(survivors) + 1)  # the all-reduce over the survivors (original rank + 1)

@@ -7,6 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 LIB=light-client-consensus-specs_amd/lcv/liblcv.so
 cp $LIB gpurun_out/.liblcv_orig.so
+trap 'cp gpurun_out/.liblcv_orig.so $LIB' EXIT  # the original library is back whatever happens
 for i in ${ROUNDS:-1 2}; do
   for v in A B; do
     cp ab/liblcv_$v.so $LIB &&

@@ -14,6 +14,7 @@ run() {  # name counters...
 run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT &&
 run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS &&
 run grbm GRBM_GUI_ACTIVE GRBM_COUNT &&
+run valu SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_CYCLES SQ_BUSY_CU_CYCLES &&
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&
 echo "pmc ok"

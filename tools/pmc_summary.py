@@ -12,6 +12,9 @@ launch over the profiled launches), with the derived quantities bench.py's roofl
                            so / 8 is the kernel's cycles; 1024 SIMDs) — the time-averaged occupancy
   lds_bank_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE  (extra cycles per LDS-array cycle)
   valu_insts_per_wave    = SQ_INSTS_VALU / SQ_WAVES
+  valu_pipe              = (SOP kernels) the SIMD cycles the launch's VALU stream needs over the launch's
+                           SIMD cycles (tools/valu_model.py: exact mad counts from the programs, measured
+                           cycles per instruction class); valu_busy above is an issue count, not this
 
     python tools/pmc_summary.py gpurun_out/pmc profiles/r02_vN/pmc.json [profiles/pmc_latest.json]
 """
@@ -70,6 +73,14 @@ def derive(c: dict) -> dict:
 
 def main(src, dst, latest=None):
     ks = {k: derive(c) for k, c in load(src).items()}
+    # the SOP kernels' VALU-pipe occupancy (tools/valu_model.py): instruction counts x measured cycles
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import valu_model
+    counts = valu_model.sop_wave_counts()
+    for k, d in ks.items():
+        p = valu_model.pipe(k, d["raw"], counts)
+        if p is not None:
+            d["valu_pipe"] = p
     doc = {"source": src, "tool": "tools/pmc_collect.sh (rocprofv3 --kernel-trace --pmc, one pass per group)",
            "kernels": ks}
     os.makedirs(os.path.dirname(dst), exist_ok=True)
@@ -79,7 +90,8 @@ def main(src, dst, latest=None):
     for k, d in ks.items():
         if k.startswith("k_sop") or k in ("k_items<F_h2c_map>", "k_items<F_sig>"):
             print(k, {x: d.get(x) for x in ("hbm_bytes_per_launch", "valu_busy", "issue_busy",
-                                              "mean_waves_per_simd", "lds_bank_conflict_rate", "valu_insts_per_wave")})
+                                              "mean_waves_per_simd", "lds_bank_conflict_rate", "valu_insts_per_wave")},
+                  (d.get("valu_pipe") or {}).get("issue_fraction"), (d.get("valu_pipe") or {}).get("pipe_utilization_upper"))
 
 
 if __name__ == "__main__":

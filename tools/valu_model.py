@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""VALU-pipe model of the SOP kernels: how many SIMD cycles a launch's vector instruction stream needs,
+and what fraction of the kernel's SIMD cycles that is — the hardware statement beside the INT32-op
+roofline (bench.py "valu_pipe").
+
+Measured on the box (tools/microbench/valubench.hip, profiles/r04_cal/valubench.txt; shader-clock cycles
+per loop iteration, W >= 2 waves per SIMD):
+  * a wave64 32-bit VALU instruction issues every ~4 SIMD cycles (69 simple ops: 296-306 cycles; the
+    intbench "71.5 T v_add_u32" of round 2 counted an add + xor that the compiler fuses into one
+    v_xad_u32: 35.8 T instructions x 64 lanes, i.e. 4.4 cycles) — 39.3 T lane-instructions/s at 2.4 GHz;
+  * a v_mad_u64_u32 takes ~6 cycles back to back (49 mads + 7 xors: 306 cycles) and ~4 when other
+    instructions sit between mads (49 mads + 84 simple ops: 543 cycles = 133 x 4.08);
+  * v_fma_f64 4.15 cycles; a 64-bit shift-add (v_lshl_add_u64) ~4-5.
+So for a launch with N_valu VALU and N_mad multiply-add wave-instructions (rocprofv3 SQ_INSTS_VALU; N_mad
+exact from the SOP programs, below):
+    issue fraction   = C_VALU * N_valu / S                        (every instruction at 4 cycles)
+    pipe upper bound = (C_VALU * N_valu + (C_MAD - C_VALU) * N_mad) / S   (every mad back to back)
+with S = GRBM_GUI_ACTIVE / 8 * 1024 the launch's SIMD cycles (GRBM summed over 8 XCDs; DVFS-true).
+
+N_mad per wave-round with K products: K * (147 + 12 mflag) + 196 [K > 0] + 12 nadd — a Karatsuba product
+is 3 x 49 mads, the 32-bit m * X scaling 12, the 14-digit Montgomery reduction 14 x 14, an add-in term's
+c * v 12 (csrc/lcv_sop.hpp, lcv_col28.hpp; `--isa` counts them in the compiled kernel).
+
+SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES ("valu_busy", 0.46-0.49 for these kernels) equals SQ_INSTS_VALU /
+SQ_WAVE_CYCLES here (one quad-cycle per instruction): the share of a resident wave's quad-cycles in which
+IT issued a VALU instruction.  With ~1.6 waves per SIMD each wave issues about every second quad-cycle, so
+the SIMD issues ~0.8 per quad-cycle: an issue count per wave, not the pipe's occupancy.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+C_VALU = 4.0   # SIMD cycles per wave64 32-bit VALU instruction (valubench: 4.08-4.3)
+C_MAD = 6.0    # SIMD cycles per wave64 v_mad_u64_u32 issued back to back (valubench: 5.7-6.0)
+SIMDS = 1024   # 256 CUs x 4 SIMDs
+
+# per-construct mad counts of the interpreter (checked against the ISA by --isa)
+MADS_PER_PRODUCT = 147      # one subtractive Karatsuba level: P0, P2 (49 unsigned each) + D (49 signed)
+MADS_MSCALE = 12            # X *= m on 12 32-bit words (rounds with mflag)
+MADS_REDC = 196             # 14 quotient digits x (1 + 13) multiply-adds
+MADS_ADDIN = 12             # add-in term c * v on 12 words
+
+# kernel name -> (gen_sop program name, items per wave)
+SOP_KERNELS = {"k_sop<F_sop_lines>": "lines", "k_sop<F_sop_acc>": "miller_acc", "k_sop<F_sop_fexp>": "fexp",
+               "k_sop<F_sop_h2c>": "h2c"}
+
+
+def sop_wave_counts() -> dict:
+    """program name -> {"mads_per_wave", "rounds", "team", "items_per_wave"} from the generator's tables."""
+    import gen_sop as G
+    out = {}
+    for p in G.build():
+        hdr, _ = p.encode()
+        mads = 0
+        for r in range(len(hdr) // 4):
+            w0 = hdr[4 * r]
+            K, nadd, mflag = w0 & 15, (w0 >> 4) & 3, (w0 >> 6) & 1
+            mads += K * (MADS_PER_PRODUCT + MADS_MSCALE * mflag) + (MADS_REDC if K else 0) + MADS_ADDIN * nadd
+        out[p.name] = {"mads_per_wave": mads, "rounds": len(hdr) // 4, "team": p.team,
+                       "items_per_wave": 64 // p.team}
+    return out
+
+
+def pipe(kernel: str, raw: dict, counts: dict | None = None, c_mad: float = C_MAD, c_valu: float = C_VALU):
+    """The VALU-pipe block of one kernel from its PMC averages per launch (raw counter dict)."""
+    if kernel not in SOP_KERNELS or not raw.get("SQ_INSTS_VALU") or not raw.get("GRBM_GUI_ACTIVE"):
+        return None
+    counts = counts or sop_wave_counts()
+    c = counts[SOP_KERNELS[kernel]]
+    waves = raw["SQ_WAVES"]
+    n_valu = raw["SQ_INSTS_VALU"]
+    n_mad = c["mads_per_wave"] * waves
+    lo = n_valu * c_valu
+    hi = lo + n_mad * (c_mad - c_valu)
+    avail = raw["GRBM_GUI_ACTIVE"] / 8 * SIMDS
+    out = {"valu_insts_per_launch": round(n_valu), "mad_insts_per_launch": round(n_mad),
+           "mad_fraction_of_valu_insts": round(n_mad / n_valu, 4),
+           "simd_cycles_per_launch": round(avail),
+           "issue_fraction": round(lo / avail, 4), "pipe_utilization_upper": round(hi / avail, 4),
+           "pipe_cycles_per_launch": round(lo), "pipe_cycles_per_launch_upper": round(hi),
+           "c_valu": c_valu, "c_mad_back_to_back": c_mad, "waves_per_launch": round(waves)}
+    if raw.get("SQ_INSTS_VALU_INT64") is not None:
+        out["int64_valu_insts_per_launch"] = round(raw["SQ_INSTS_VALU_INT64"])
+    return out
+
+
+def check_isa(asm_path: str) -> dict:
+    """Count v_mad_u64_u32 / v_mad_i64_i32 in the SOP kernels' product loop and round tail of a
+    `hipcc --cuda-device-only -S` listing of csrc/lcv_k_sop.hip; returns the counts per kernel."""
+    import re
+    text = open(asm_path).read().split("\n")
+    out, cur = {}, None
+    for line in text:
+        m = re.match(r"^(_Z5k_sopI\w+):", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = {"v_mad_u64_u32": 0, "v_mad_i64_i32": 0}
+        elif cur and line.strip().startswith(("v_mad_u64_u32", "v_mad_i64_i32")):
+            out[cur][line.split()[0]] += 1
+        elif cur and "s_endpgm" in line:
+            cur = None
+    return out
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--isa":
+        print(json.dumps(check_isa(sys.argv[2]), indent=1))
+    elif len(sys.argv) > 1:
+        doc = json.load(open(sys.argv[1]))
+        cnt = sop_wave_counts()
+        for k, d in doc["kernels"].items():
+            p = pipe(k, d["raw"], cnt)
+            if p:
+                print(k, json.dumps(p))
+    else:
+        print(json.dumps(sop_wave_counts(), indent=1))
