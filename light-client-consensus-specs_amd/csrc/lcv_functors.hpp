@@ -149,14 +149,15 @@ struct F_export_g1 {
     fp_to_be48(out + 96 * (size_t)i + 48, y);
   }
 };
-struct F_export_fp12 {
+struct F_export_fp12 {  // W.f (item-major, coefficient order w^0 .. w^5, f12_ld_coeff) -> big-endian bytes
   const uint32_t* base; uint32_t cap; uint8_t* out;
   LCV_HD void operator()(uint32_t i) const {
-    fp12 f;
-    soa_ld_fp12(f, base, cap, i);
-    const fp2* g[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
     uint8_t* o = out + 576 * (size_t)i;
-    for (int k = 0; k < 6; ++k) { fp_to_be48(o + 96 * k, g[k]->c0); fp_to_be48(o + 96 * k + 48, g[k]->c1); }
+    for (uint32_t s = 0; s < 12; ++s) {
+      fp x;
+      f12_ld_coeff(x.v, base, i, s);
+      fp_to_be48(o + 48 * s, x);
+    }
   }
 };
 struct F_import_pq {  // debug pairing inputs: P -> W.pk, Q -> W.qh (no validation: test entry point)

@@ -110,45 +110,48 @@ struct F_sop_acc {
   }
   LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {  // slot 2g + c -> W.f
     for (uint32_t s = lane; s < 12; s += TEAM) {
-      fp x;
-      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = lds[12 * s + j];
-      soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(s >> 1) + (s & 1u), x);
+      uint32_t x[12];
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x[j] = lds[12 * s + j];
+      f12_st_coeff(W.f, i, s, x);
     }
   }
 };
 
 struct F_sop_fexp {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 2;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
-  static_assert(LCV_SOP_FEXP_SLOT_R5_1 == LCV_SOP_FEXP_SLOT_R0_0 + 11, "r in consecutive slots");
+  // the result's 12 coefficients (slot order 2 g + c; the generator places them anywhere)
+  static constexpr uint32_t RS[12] = {LCV_SOP_FEXP_SLOT_R0_0, LCV_SOP_FEXP_SLOT_R0_1, LCV_SOP_FEXP_SLOT_R1_0,
+                                      LCV_SOP_FEXP_SLOT_R1_1, LCV_SOP_FEXP_SLOT_R2_0, LCV_SOP_FEXP_SLOT_R2_1,
+                                      LCV_SOP_FEXP_SLOT_R3_0, LCV_SOP_FEXP_SLOT_R3_1, LCV_SOP_FEXP_SLOT_R4_0,
+                                      LCV_SOP_FEXP_SLOT_R4_1, LCV_SOP_FEXP_SLOT_R5_0, LCV_SOP_FEXP_SLOT_R5_1};
   LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
   LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
   LCV_HD void prologue(uint32_t i, uint32_t lane, uint32_t* lds) const {
     for (uint32_t s = lane; s < 12; s += TEAM) {
-      fp x;
-      soa_ld_fp(x, W.f, W.cap, i, 2 * fp12_soa_slot(s >> 1) + (s & 1u));
-      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * s + j] = x.v[j];
+      uint32_t x[12];
+      f12_ld_coeff(x, W.f, i, s);
+      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * s + j] = x[j];
     }
   }
   // the pairing value (e^3) to W.f; "== 1" to W.pair_ok
   LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {
-    const uint32_t* r = lds + 12 * LCV_SOP_FEXP_SLOT_R0_0;
     for (uint32_t s = lane; s < 12; s += TEAM) {
-      fp x;
-      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = r[12 * s + j];
-      soa_st_fp(W.f, W.cap, i, 2 * fp12_soa_slot(s >> 1) + (s & 1u), x);
+      uint32_t x[12];
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x[j] = lds[12 * RS[s] + j];
+      f12_st_coeff(W.f, i, s, x);
     }
     if (lane == 0) {
       fp x, one;
-      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = r[j];
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x.v[j] = lds[12 * RS[0] + j];
       fp_one(one);
       bool ok = fp_eq(x, one);
       for (uint32_t k = 1; k < 12; ++k) {
         uint32_t z = 0;
-        for (int j = 0; j < 12; ++j) z |= r[12 * k + j];
+        for (int j = 0; j < 12; ++j) z |= lds[12 * RS[k] + j];
         ok = ok && z == 0;
       }
       W.pair_ok[i] = ok ? 1 : 0;

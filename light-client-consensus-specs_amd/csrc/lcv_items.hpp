@@ -94,6 +94,30 @@ LCV_FN void soa_ld_fp(fp& r, const uint32_t* base, size_t cap, size_t i, size_t 
 LCV_FN void soa_st_fp(uint32_t* base, size_t cap, size_t i, size_t slot, const fp& a) {
   LCV_UNROLL for (int k = 0; k < 12; ++k) base[(slot * 12 + k) * cap + i] = a.v[k];
 }
+// W.f (the Miller loop's output, the final exponentiation's e^3): item-major, the 12 Fp coefficients of
+// item i in the SOP programs' slot order (2 g + c for the w^g coefficient, component c), 48 contiguous
+// bytes each, so a team's lanes move their coefficients as 16-byte accesses of one 576-byte row
+LCV_FN void f12_st_coeff(uint32_t* base, size_t i, uint32_t s, const uint32_t v[12]) {
+  uint32_t* d = base + (i * 12 + s) * 12;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint4* q = (uint4*)d;
+  LCV_UNROLL for (int k = 0; k < 3; ++k) q[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+#else
+  LCV_UNROLL for (int k = 0; k < 12; ++k) d[k] = v[k];
+#endif
+}
+LCV_FN void f12_ld_coeff(uint32_t v[12], const uint32_t* base, size_t i, uint32_t s) {
+  const uint32_t* d = base + (i * 12 + s) * 12;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* q = (const uint4*)d;
+  LCV_UNROLL for (int k = 0; k < 3; ++k) {
+    const uint4 t = q[k];
+    v[4 * k] = t.x; v[4 * k + 1] = t.y; v[4 * k + 2] = t.z; v[4 * k + 3] = t.w;
+  }
+#else
+  LCV_UNROLL for (int k = 0; k < 12; ++k) v[k] = d[k];
+#endif
+}
 LCV_FN void soa_ld_fp2(fp2& r, const uint32_t* base, size_t cap, size_t i, size_t slot) {
   soa_ld_fp(r.c0, base, cap, i, 2 * slot);
   soa_ld_fp(r.c1, base, cap, i, 2 * slot + 1);

@@ -92,6 +92,11 @@ class Op:
         self.dst = dst
         # a negative multiplier is folded into X's term signs: m > 0 from here on
         self.prods = [(list(x) if m > 0 else [~t for t in x], list(y), abs(int(m))) for x, y, m in prods]
+        # a product with a single constant factor takes the whole sign on the constant (p - c is another
+        # constant): the variable's value then needs no shadow slot for this read
+        self.prods = [([~t for t in x], [~y[0]], m) if (len(y) == 1 and isinstance(y[0].slot, tuple) and x and
+                                                       all(t.neg for t in x)) else (x, y, m)
+                      for x, y, m in self.prods]
         self.adds = [(s if isinstance(s, tuple) else int(s), int(c)) for s, c in adds]
         self.kind = kind
         self.load = load    # (ld_slot, io index): side-load of an Fp value from the program's input stream
@@ -538,12 +543,18 @@ class Program:
 
 
 # ============================================================================ formula helpers
-def fp2_prod(x, y, comp, xi=False, m=1):
-    """Products of component `comp` of (xi *) x*y for Fp2 views x = (x0, x1), y = (y0, y1)."""
+def fp2_prod(x, y, comp, xi=False, m=1, negx=False):
+    """Products of component `comp` of (xi *) x*y for Fp2 views x = (x0, x1), y = (y0, y1).
+    negx: the xi forms read negated terms of x only, (x0 - x1) y0 - (x0 + x1) y1 and
+    (x0 + x1) y0 + (x0 - x1) y1 (so only x's values need shadow slots: Program.apply_shadows)."""
     x0, x1 = x
     y0, y1 = y
     if not xi:
         return [([x0], [y0], m), ([~x1], [y1], m)] if comp == 0 else [([x0], [y1], m), ([x1], [y0], m)]
+    if negx:
+        if comp == 0:
+            return [([x0, ~x1], [y0], m), ([~x0, ~x1], [y1], m)]
+        return [([x0, x1], [y0], m), ([x0, ~x1], [y1], m)]
     if comp == 0:   # x0 (y0 - y1) - x1 (y0 + y1)
         return [([x0], [y0, ~y1], m), ([~x1], [y0, y1], m)]
     return [([x0], [y0, y1], m), ([x1], [y0, ~y1], m)]
@@ -603,15 +614,22 @@ def fp12_sqr_ops(f, out):
     return ops
 
 
-def fp12_mul_ops(a, b, out):
-    """out = a*b (dense, schoolbook over Fp2): 12 ops, 12 products each."""
+def fp12_mul_ops(a, b, out, negx=False, conj_out=False):
+    """out = a*b (dense, schoolbook over Fp2): 12 ops, 12 products each.  negx: negated reads of a only
+    (a single-term y read negated through a view moves its sign to x); conj_out: out = conj(a*b) (the
+    odd coefficients' products negated, on x)."""
     ops = []
     for k in range(6):
         for comp in range(2):
             prods = []
             for i in range(6):
                 j = (k - i) % 6
-                prods += fp2_prod(a[i], b[j], comp, xi=(i + j >= 6))
+                prods += fp2_prod(a[i], b[j], comp, xi=(i + j >= 6), negx=negx)
+            if conj_out and k % 2:
+                prods = [(x, y, -m) for x, y, m in prods]
+            if negx:
+                prods = [(x if not (len(y) == 1 and y[0].neg) else [~t for t in x], [~y[0]] if len(y) == 1 and y[0].neg else y, m)
+                         for x, y, m in prods]
             ops.append(Op(dst_of(out[k][comp]), prods))
     return ops
 
@@ -853,7 +871,7 @@ def frob_ops(p, a, k, out):
     return ops
 
 
-def fexp_program(team=12):
+def fexp_program_r03(team=12):
     """f^((p^12 - 1)/r) * 3 (result e^3): easy part
     (p^6 - 1)(p^2 + 1) with a team-parallel Fp12 inversion, hard part (x-1)^2 (x+p)(x^2+p^2-1) + 3."""
     p = Program("fexp", team)
@@ -960,6 +978,129 @@ def fexp_program(team=12):
     for i in range(6):
         for c in range(2):
             p.named[f"r{i}_{c}"] = m[i][c].slot
+    return p
+
+
+def fexp_program(team=12):
+    """f^((p^12 - 1)/r) * 3 (result e^3), three live Fp12 values in the hard part (r04): easy part
+    (p^6 - 1)(p^2 + 1) with a team-parallel Fp12 inversion whose temporaries are released as soon as
+    they die, then with m = f^((p^6 - 1)(p^2 + 1)), x < 0, e() = exponentiation by |x| (e(a) = a^-x):
+        F2 = m^3 (cyclotomic square times m, once, first)
+        A  = conj(e(m) m) = m^(x - 1)                  (into m's slots, conjugated by the products)
+        A2 = conj(e(A) A) = m^((x - 1)^2)               (in place)
+        Bv = conj(e(A2)) frob1(A2) = A2^(x + p)          (frob1 in place, then the product)
+        F2 = F2 frob2(Bv) conj(Bv);  F3 = e(Bv);  F1 = e(F3)
+        r  = F1 F2 = Bv^(x^2 + p^2 - 1) m^3              (the r03 order's value, fexp_program_r03)
+    Every product reads negated values only on its x side (fp2_prod negx, the exponentiation's running
+    value), so the chains' bases need no shadow slots: LDS per item 79 -> fewer slots, a third wave per
+    SIMD."""
+    p = Program("fexp", team)
+    f = fp12_slots(p, "f")
+    c0 = [f[0], f[2], f[4]]   # Fp6 halves in the v basis
+    c1 = [f[1], f[3], f[5]]
+    rel = lambda vs: p.release([x.slot for v in vs for x in (v if isinstance(v, tuple) else (v,))])  # noqa: E731
+    # ---- t = c0^2 - v c1^2
+    t = [slots2(p) for _ in range(3)]
+    ops = []
+    for comp in range(2):
+        a, b = c0, c1
+        ops.append(Op(dst_of(t[0][comp]), fp2_sqr(a[0], comp) + fp2_prod(a[1], a[2], comp, True, 2) +
+                      fp2_sqr(b[1], comp, True, -1) + fp2_prod(b[0], b[2], comp, True, -2)))
+        ops.append(Op(dst_of(t[1][comp]), fp2_prod(a[0], a[1], comp, False, 2) + fp2_sqr(a[2], comp, True) +
+                      fp2_sqr(b[0], comp, False, -1) + fp2_prod(b[1], b[2], comp, True, -2)))
+        ops.append(Op(dst_of(t[2][comp]), fp2_sqr(a[1], comp) + fp2_prod(a[0], a[2], comp, False, 2) +
+                      fp2_prod(b[0], b[1], comp, False, -2) + fp2_sqr(b[2], comp, True, -1)))
+    p.round(ops)
+    # ---- s = adj(t): s0 = t0^2 - xi t1 t2, s1 = xi t2^2 - t0 t1, s2 = t1^2 - t0 t2
+    s_ = [slots2(p) for _ in range(3)]
+    ops = []
+    for comp in range(2):
+        ops.append(Op(dst_of(s_[0][comp]), fp2_sqr(t[0], comp) + fp2_prod(t[1], t[2], comp, True, -1)))
+        ops.append(Op(dst_of(s_[1][comp]), fp2_sqr(t[2], comp, True) + fp2_prod(t[0], t[1], comp, False, -1)))
+        ops.append(Op(dst_of(s_[2][comp]), fp2_sqr(t[1], comp) + fp2_prod(t[0], t[2], comp, False, -1)))
+    p.round(ops)
+    # ---- d = t0 s0 + xi (t2 s1 + t1 s2)
+    d = slots2(p)
+    p.round([Op(dst_of(d[c]), fp2_prod(t[0], s_[0], c) + fp2_prod(t[2], s_[1], c, True) +
+                fp2_prod(t[1], s_[2], c, True)) for c in range(2)])
+    rel(t)
+    # ---- n = d0^2 + d1^2 ; ninv
+    n = T(p.alloc())
+    p.round([Op(n.slot, [([d[0]], [d[0]], 1), ([d[1]], [d[1]], 1)])])
+    ninv = T(p.alloc())
+    p.round([Op(ninv.slot, [], [(n.slot, 1)], kind="inv")])
+    rel([n])
+    # ---- dinv = (d0 ninv, -d1 ninv) ; tinv = s * dinv
+    dinv = slots2(p)
+    p.round([Op(dst_of(dinv[0]), [([d[0]], [ninv], 1)]), Op(dst_of(dinv[1]), [([d[1]], [ninv], -1)])])
+    rel([d, ninv])
+    ti = [slots2(p) for _ in range(3)]
+    p.round([Op(dst_of(ti[i][c]), fp2_prod(s_[i], dinv, c)) for i in range(3) for c in range(2)])
+    rel(s_ + [dinv])
+    # ---- finv = (c0 * ti, -c1 * ti)   (Fp6 products)
+    fi = fp12_slots(p)
+    fi0 = [fi[0], fi[2], fi[4]]
+    fi1 = [fi[1], fi[3], fi[5]]
+    ops = []
+    for half, src, sign in ((fi0, c0, 1), (fi1, c1, -1)):
+        for k in range(3):
+            for comp in range(2):
+                prods = []
+                for i in range(3):
+                    j = (k - i) % 3
+                    prods += fp2_prod(src[i], ti[j], comp, xi=(i + j >= 3), m=sign)
+                ops.append(Op(dst_of(half[k][comp]), prods))
+    p.round(ops)
+    rel(ti)
+    # ---- t1 = conj(f) * finv (in place over finv) ; m = frob2(t1) * t1 (frob2 into f's slots, m in place)
+    p.round(fp12_mul_ops(conj12(f), fi, fi))
+    t1 = fi
+    p.round(frob_ops(p, t1, 2, f))
+    p.round(fp12_mul_ops(f, t1, t1))
+    m = t1
+    for i in range(6):
+        for c in range(2):
+            p.named[f"m{i}_{c}"] = m[i][c].slot
+    rel(flat12(f))
+    F1 = m
+    F2 = fp12_slots(p)
+    F3 = fp12_slots(p)
+
+    def exp_x(a, out):
+        """out = a^|x| (a cyclotomic; `out` must differ from a's slots); negated reads on out only."""
+        firstsq = True
+        for bit in bin(X_ABS)[3:]:
+            p.round(cyclo_sqr_ops(a if firstsq else out, out))
+            firstsq = False
+            if bit == "1":
+                p.round(fp12_mul_ops(out, a, out, negx=True))
+
+    # F2 = m^3 (negated reads on m, whose shadows the squarings need anyway)
+    p.round(cyclo_sqr_ops(F1, F2))
+    p.round(fp12_mul_ops(F1, F2, F2, negx=True))
+    # A = conj(e(m) m) into F1
+    exp_x(F1, F3)
+    p.round(fp12_mul_ops(F3, F1, F1, negx=True, conj_out=True))
+    # A2 = conj(e(A) A) into F1
+    exp_x(F1, F3)
+    p.round(fp12_mul_ops(F3, F1, F1, negx=True, conj_out=True))
+    # Bv = conj(e(A2)) frob1(A2) into F1
+    exp_x(F1, F3)
+    p.round(frob_ops(p, F1, 1, F1))
+    p.round(fp12_mul_ops(conj12(F3), F1, F1, negx=True))
+    # F3 = frob2(Bv) conj(Bv) (conj's signs on F3's reads); F2 = m^3 F3; Bv re-stored (a product-free
+    # copy round: its negated shadows are written there, just before the chain's first squaring reads
+    # them, instead of living from Bv's product through these rounds); F3 = e(Bv); F1 = e(F3); r = F1 F2
+    p.round(frob_ops(p, F1, 2, F3))
+    p.round(fp12_mul_ops(F3, conj12(F1), F3, negx=True))
+    p.round(fp12_mul_ops(F3, F2, F2, negx=True))
+    p.round(copy_ops(flat12(F1), flat12(F1)))
+    exp_x(F1, F3)
+    exp_x(F3, F1)
+    p.round(fp12_mul_ops(F1, F2, F2, negx=True))
+    for i in range(6):
+        for c in range(2):
+            p.named[f"r{i}_{c}"] = F2[i][c].slot
     return p
 
 

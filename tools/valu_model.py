@@ -68,13 +68,19 @@ def sop_wave_counts() -> dict:
 
 def pipe(kernel: str, raw: dict, counts: dict | None = None, c_mad: float = C_MAD, c_valu: float = C_VALU):
     """The VALU-pipe block of one kernel from its PMC averages per launch (raw counter dict)."""
-    if kernel not in SOP_KERNELS or not raw.get("SQ_INSTS_VALU") or not raw.get("GRBM_GUI_ACTIVE"):
+    if not raw.get("SQ_INSTS_VALU") or not raw.get("GRBM_GUI_ACTIVE") or not kernel.startswith("k_"):
         return None
-    counts = counts or sop_wave_counts()
-    c = counts[SOP_KERNELS[kernel]]
     waves = raw["SQ_WAVES"]
     n_valu = raw["SQ_INSTS_VALU"]
-    n_mad = c["mads_per_wave"] * waves
+    if kernel in SOP_KERNELS:
+        counts = counts or sop_wave_counts()
+        n_mad = counts[SOP_KERNELS[kernel]]["mads_per_wave"] * waves
+        mad_source = "exact: the SOP program tables"
+    elif raw.get("SQ_INSTS_VALU_INT64") is not None:
+        n_mad = raw["SQ_INSTS_VALU_INT64"]  # v_mad_u64_u32 are INT64 instructions (valubench)
+        mad_source = "SQ_INSTS_VALU_INT64 (includes the 64-bit shifts / adds: an upper bound)"
+    else:
+        return None
     lo = n_valu * c_valu
     hi = lo + n_mad * (c_mad - c_valu)
     avail = raw["GRBM_GUI_ACTIVE"] / 8 * SIMDS
@@ -83,7 +89,8 @@ def pipe(kernel: str, raw: dict, counts: dict | None = None, c_mad: float = C_MA
            "simd_cycles_per_launch": round(avail),
            "issue_fraction": round(lo / avail, 4), "pipe_utilization_upper": round(hi / avail, 4),
            "pipe_cycles_per_launch": round(lo), "pipe_cycles_per_launch_upper": round(hi),
-           "c_valu": c_valu, "c_mad_back_to_back": c_mad, "waves_per_launch": round(waves)}
+           "c_valu": c_valu, "c_mad_back_to_back": c_mad, "waves_per_launch": round(waves),
+           "mad_count_source": mad_source}
     if raw.get("SQ_INSTS_VALU_INT64") is not None:
         out["int64_valu_insts_per_launch"] = round(raw["SQ_INSTS_VALU_INT64"])
     return out
