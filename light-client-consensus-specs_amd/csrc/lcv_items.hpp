@@ -75,7 +75,7 @@ struct Work {
   uint8_t* sig_status;   // [cap]
   uint32_t* pk;          // [24][cap] aggregate pubkey affine
   uint8_t* agg_status;   // [cap]
-  uint32_t* f;           // [144][cap]   Miller output, then the pairing value
+  uint32_t* f;           // [cap][144]   Miller output, then the pairing value (item-major: f12_st_coeff)
   uint8_t* pair_ok;      // [cap]
   uint8_t* verdict;      // [cap]
   uint8_t* reason;       // [cap]

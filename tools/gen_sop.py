@@ -151,7 +151,7 @@ class Program:
         lane), unless that order would read a slot an earlier part wrote; then the given order."""
         ops = [o for o in ops if o is not None]
         assert ops
-        dsts = [o.dst for o in ops] + [o.load[0] for o in ops if o.load]
+        dsts = [o.dst for o in ops if o.dst is not None] + [o.load[0] for o in ops if o.load]
         assert len(dsts) == len(set(dsts)), "two ops of a round write one slot"
 
         def parts(order):
@@ -434,7 +434,9 @@ class Program:
                     continue
                 o = ops[lane]
                 flags = (1 if o.kind == "inv" else 0) | (2 if o.load else 0) | (4 if o.emit is not None else 0)
-                w[0] = self.sl(o.dst) | flags << 12 | ((self.sl(o.load[0]) if o.load else 0) << 16)
+                # dst None: an emit-only op (its value leaves through the output stream, no slot)
+                dst_enc = SLOT_MASK if o.dst is None else self.sl(o.dst)
+                w[0] = dst_enc | flags << 12 | ((self.sl(o.load[0]) if o.load else 0) << 16)
                 io = (o.load[1] if o.load else o.emit if o.emit is not None else 0)
                 assert 0 <= io < 4096
                 ds = SHADOW_NONE if o.dst_shadow is None else o.dst_shadow
@@ -526,7 +528,8 @@ class Program:
                         writes.append((lsh, P - io_in[io]))
                 if flags & 4:
                     io_out[io] = res
-                writes.append((dst, res))
+                if dst != SLOT_MASK:
+                    writes.append((dst, res))
                 if shadow and dsh != SHADOW_NONE:
                     writes.append((dsh, P - res))
             for s, v in writes:
@@ -704,7 +707,7 @@ def line_program(team=10):
     B, Cp, J, XY, YZ = (slots2(p) for _ in range(5))
     BmF, BpF = slots2(p), slots2(p)
     C48 = slots2(p)  # 48 C': carries most of 1728 = 36 * 48, so no scaled operand of the T update needs a 15th limb
-    la, lb, lc = slots2(p), slots2(p), slots2(p)
+    # the line values (a, b, c) only leave through the output stream: emit-only ops without LDS slots (r04)
     # the addition step's temporaries reuse the doubling step's (different steps, sequential rounds)
     th, lam, Cc, D, E, F, G = B, Cp, J, XY, YZ, BmF, BpF
     H, GmH = slots2(p), slots2(p)
@@ -732,7 +735,7 @@ def line_program(team=10):
         # round-one values, ride in the next round's idle lanes (it has 6 ops of K = 2 on 10 lanes)
         ops = [Op(dst_of(BmF[c]), [], [(B[c].slot, 1), (Cp[c].slot, -36)]) for c in range(2)]
         ops += [Op(dst_of(BpF[c]), [], [(B[c].slot, 1), (Cp[c].slot, 36)]) for c in range(2)]
-        ops += [Op(dst_of(la[c]), [], [(B[c].slot, 1), (Cp[c].slot, -12)], emit=6 * step + c) for c in range(2)]
+        ops += [Op(None, [], [(B[c].slot, 1), (Cp[c].slot, -12)], emit=6 * step + c) for c in range(2)]
         ops += [Op(dst_of(C48[c]), [], [(Cp[c].slot, 48)]) for c in range(2)]
         p.round(ops)
         # T: X = 2 XY (B - 3E), Y = (B + 3E)^2 - 1728 C'^2, Z = 8 B YZ, with 1728 C'^2 taken as
@@ -742,22 +745,23 @@ def line_program(team=10):
         ops = [Op(dst_of(X[c]), fp2_prod(XY, BmF, c, m=2)) for c in range(2)]
         ops += [Op(dst_of(Y[c]), fp2_sqr(BpF, c) + ysq[c]) for c in range(2)]
         ops += [Op(dst_of(Z[c]), fp2_prod(B, YZ, c, m=8)) for c in range(2)]
-        ops += [Op(dst_of(lb[c]), [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
-        ops += [Op(dst_of(lc[c]), [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
+        ops += [Op(None, [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
+        ops += [Op(None, [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
         p.round(ops)
         step += 1
         if bit == "1":
             # ---- addition T + Q: theta = Y - qy Z, lam = X - qx Z
-            ops = [Op(dst_of(th[c]), fp2_prod(qy, Z, c, m=-1), [(Y[c].slot, 1)]) for c in range(2)]
-            ops += [Op(dst_of(lam[c]), fp2_prod(qx, Z, c, m=-1), [(X[c].slot, 1)]) for c in range(2)]
+            # (Z on the x side: the negated reads fall on the walk's running value, Q needs no shadows)
+            ops = [Op(dst_of(th[c]), fp2_prod(Z, qy, c, m=-1), [(Y[c].slot, 1)]) for c in range(2)]
+            ops += [Op(dst_of(lam[c]), fp2_prod(Z, qx, c, m=-1), [(X[c].slot, 1)]) for c in range(2)]
             p.round(ops)
             # C = theta^2, D = lam^2; line (theta qx - lam qy, theta * nxP, lam * yP)
             ops = [Op(dst_of(Cc[c]), fp2_sqr(th, c)) for c in range(2)]
             ops += [Op(dst_of(D[c]), fp2_sqr(lam, c)) for c in range(2)]
-            ops += [Op(dst_of(la[c]), fp2_prod(th, qx, c) + fp2_prod(lam, qy, c, m=-1), emit=6 * step + c)
+            ops += [Op(None, fp2_prod(th, qx, c) + fp2_prod(lam, qy, c, m=-1), emit=6 * step + c)
                     for c in range(2)]
-            ops += [Op(dst_of(lb[c]), [([th[c]], [nxP], 1)], emit=6 * step + 2 + c) for c in range(2)]
-            ops += [Op(dst_of(lc[c]), [([lam[c]], [yP], 1)], emit=6 * step + 4 + c) for c in range(2)]
+            ops += [Op(None, [([th[c]], [nxP], 1)], emit=6 * step + 2 + c) for c in range(2)]
+            ops += [Op(None, [([lam[c]], [yP], 1)], emit=6 * step + 4 + c) for c in range(2)]
             p.round(ops)
             # E = lam D, F = Z C, G = X D
             ops = [Op(dst_of(E[c]), fp2_prod(lam, D, c)) for c in range(2)]
@@ -774,9 +778,10 @@ def line_program(team=10):
             ops += [Op(dst_of(Z[c]), fp2_prod(Z, E, c)) for c in range(2)]
             p.round(ops)
             step += 1
+    p.release([v.slot for f2 in (B, Cp, J, XY, YZ, BmF, BpF, C48, H, GmH) for v in f2])
     e1, e2 = slots2(p, "e1"), slots2(p, "e2")
-    p.round([Op(dst_of(e1[c]), fp2_prod(px, Z, c), [(X[c].slot, -1)]) for c in range(2)] +
-            [Op(dst_of(e2[c]), fp2_prod(py, Z, c), [(Y[c].slot, 1)]) for c in range(2)])
+    p.round([Op(dst_of(e1[c]), fp2_prod(Z, px, c), [(X[c].slot, -1)]) for c in range(2)] +
+            [Op(dst_of(e2[c]), fp2_prod(Z, py, c), [(Y[c].slot, 1)]) for c in range(2)])
     p.nsteps = step
     return p
 
@@ -1138,8 +1143,8 @@ class G2Ops:
 
     def __init__(self, p):
         self.p = p
-        self.t = [slots2(p) for _ in range(6)]   # round-1 products
-        self.u = [slots2(p) for _ in range(4)]   # round-2 linear combinations
+        self.t = [slots2(p) for _ in range(6)]   # round-1 products (round 2 overwrites them in place)
+        self.u = None
         self.one = T(p.const(1))
 
     def dbl(self, P, out):
@@ -1178,7 +1183,9 @@ class G2Ops:
         ops += [Op(dst_of(t4[c]), fp2_prod(Y1, Z2, c) + fp2_prod(Z1, Y2, c)) for c in range(2)]
         ops += [Op(dst_of(y3[c]), fp2_prod(X1, Z2, c) + fp2_prod(Z1, X2, c)) for c in range(2)]
         p.round(ops)
-        z3, t1m, y3b, x3t = self.u
+        # round 2 writes over round 1's values in place (every read of a round precedes its stores):
+        # z3 over t1, t1m over t2, y3b over y3, x3t over t0 — no separate temporaries (r04)
+        z3, t1m, y3b, x3t = (t1, t2, y3, t0) if self.u is None else self.u
         one = self.one
         # b3 v = 12 (1 + u) v: (12 v0 - 12 v1, 12 v0 + 12 v1)
         p.round([Op(dst_of(z3[0]), [([t1[0]], [one], 1)], [(t2[0].slot, 12), (t2[1].slot, -12)]),
@@ -1259,22 +1266,23 @@ def h2c_program(team=8):
     p.round([o for k in range(2) for o in poly_ops(k, XN, xn[k]) + poly_ops(k, YN, yn[k])] +
             [o for k in range(2) for o in poly_ops(k, XD, xd[k])])
     p.round([o for k in range(2) for o in poly_ops(k, YD, yd[k])])
+    # (r04) the isogeny's temporaries are released as they die, so the points reuse their slots
+    p.release([v.slot for grp in (x2, x3) for f2 in grp for v in f2] + [v.slot for pt in m for v in pt[0]])
     q = [g2_slots(p) for _ in range(2)]
     yyn = [slots2(p) for _ in range(2)]
     p.round([Op(dst_of(q[k][0][c]), fp2_prod(xn[k], yd[k], c)) for k in range(2) for c in range(2)] +
             [Op(dst_of(q[k][2][c]), fp2_prod(xd[k], yd[k], c)) for k in range(2) for c in range(2)] +
             [Op(dst_of(yyn[k][c]), fp2_prod(m[k][1], yn[k], c)) for k in range(2) for c in range(2)])
     p.round([Op(dst_of(q[k][1][c]), fp2_prod(yyn[k], xd[k], c)) for k in range(2) for c in range(2)])
-    p.release([v.slot for grp in (x2, x3, xn, xd, yn, yd, yyn) for f2 in grp for v in f2] +
-              [v.slot for pt in m for f2 in pt for v in f2])
+    p.release([v.slot for grp in (xn, xd, yn, yd, yyn) for f2 in grp for v in f2] +
+              [v.slot for pt in m for v in pt[1]])
     g = G2Ops(p)
     Pt = g2_slots(p)
     g.add(q[0], q[1], Pt)
-    # clear_cofactor: t1 = -[|x|]Pt, t2 = psi(Pt), t3 = psi^2(2 Pt) - t2, t2 = -[|x|](t1 + t2),
-    # Q = t3 + t2 - t1 - Pt
-    A = g2_slots(p)
-    g.mul_xabs(Pt, A)
-    t1 = g2_neg_view(A)
+    # clear_cofactor (RFC 9380 G.3): Q = [x^2 - x - 1] Pt + [x - 1] psi(Pt) + psi^2(2 Pt), with A = [|x|] Pt:
+    #   t2 = psi(Pt);  t3 = psi^2(2 Pt) - t2;  t3 = (A + t3) ... u = Pt - t3;  t2 = t2 - A;  -Q = u + [|x|] t2
+    # (r04 order) the psi terms first, then the chains; every addition takes the value it just made as P1
+    # (its negated reads land on that value's shadows) and Pt / A die before the second chain
     t2 = q[0]                       # q0, q1 are dead after Pt
     g.psi(Pt, t2)
     t3 = q[1]
@@ -1282,13 +1290,17 @@ def h2c_program(team=8):
     g.psi(t3, t3)
     g.psi(t3, t3)
     g.add(t3, g2_neg_view(t2), t3)
-    g.add(t1, t2, t2)
+    A = g2_slots(p)
+    g.mul_xabs(Pt, A)
+    g.add(A, t3, t3)
+    g.add(g2_neg_view(t3), Pt, t3)  # u = Pt - (psi^2(2 Pt) - psi(Pt) + A)
+    g.add(g2_neg_view(A), t2, t2)   # t2 = psi(Pt) - A
+    p.release([v.slot for pt in (Pt, A) for f2 in pt for v in f2])
     B = g2_slots(p)
     g.mul_xabs(t2, B)
-    g.add(t3, g2_neg_view(B), t3)
-    g.add(t3, g2_neg_view(t1), t3)
-    g.add(t3, g2_neg_view(Pt), t3)
-    X, Y, Z = t3
+    g.add(B, t3, t3)                 # w = u + [|x|] t2 = -Q
+    p.release([v.slot for pt in (t2, B) for f2 in pt for v in f2] + [v.slot for f2 in g.t for v in f2])
+    X, Y, Z = g2_neg_view(t3)
     # affine: zi = Z^-1 via the norm
     n, ninv = T(p.alloc()), T(p.alloc())
     p.round([Op(n.slot, [([Z[0]], [Z[0]], 1), ([Z[1]], [Z[1]], 1)])])
