@@ -9,6 +9,9 @@
 #include "lcv_functors.hpp"
 #include "lcv_sop.hpp"
 #include "lcv_sop_programs.inc"
+#if defined(LCV_KERNEL_UNIT)
+#include "lcv_sop_quad.hpp"
+#endif
 
 enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
 // per-item LDS pitch = 12 * slots + SOP_PITCH_PAD words: 4 keeps every value 16-byte aligned for the
@@ -239,5 +242,42 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
     __syncthreads();
   }
   if (active) f.epilogue(item, lane, my);
+}
+
+// The quad engine's round loop (lcv_sop_quad.hpp; latency mode): ONE item per one-wave block, op o of a
+// round on lanes 4o .. 4o + 3 (TEAM <= 16).  LDS: the constants, the item's slots, then per op the
+// 4 x 29 64-bit column scratch of the products' transpose (zeroed once: each lane rewrites the same
+// positions every round, the rest stays zero).
+template <class F>
+__global__ __launch_bounds__(64) void k_sop_quad(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM;
+  static_assert(T <= 16, "four lanes per op in one wave");
+  constexpr uint32_t ITEM_WORDS = (F::LDS_WORDS + 1u) & ~1u;  // 8-byte aligned scratch after the slots
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t op = threadIdx.x >> 2, q = threadIdx.x & 3u;
+  const uint32_t item = blockIdx.x;
+  const bool active = op < T && item < n;
+  uint32_t* my = lds + F::SHARED_WORDS;
+  uint64_t* scratch = (uint64_t*)(lds + F::SHARED_WORDS + ITEM_WORDS);
+  uint64_t* S = scratch + (op < T ? op : 0) * lcv::QUAD_SCRATCH_U64;
+  for (uint32_t k = threadIdx.x; k < F::SHARED_WORDS; k += 64) lds[k] = f.P.consts[k];
+  for (uint32_t k = threadIdx.x; k < T * lcv::QUAD_SCRATCH_U64; k += 64) scratch[k] = 0;
+  if (active && q == 0) f.prologue(item, op, my);
+  __syncthreads();
+  uint32_t pz[16];
+  lcv::quad_ptable(pz, q);
+  const uint32_t* io_in = active ? f.io_in(item) : nullptr;
+  uint32_t* io_out = active ? f.io_out(item) : nullptr;
+  const uint32_t R = f.P.rounds, ns = f.P.nslots;
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
+    const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 1]);
+    const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
+    const uint32_t h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 3]);
+    const uint32_t* w = f.P.rec + off + (active ? op : 0) * words;
+    if (active) lcv::sop_exec_quad(h0, h3, w, lcv::sop_pre(h0, w), my, my, lds, ns, io_in, io_out, q, S, pz);
+    __syncthreads();
+  }
+  if (active && q == 0) f.epilogue(item, op, my);
 }
 #endif
