@@ -526,9 +526,9 @@ def latency_lines(v, sb, calls: int = 20) -> dict:
         t0 = time.perf_counter()
         fav_ok &= v.fast_aggregate_verify(pks, msg, sig)
         tf.append(time.perf_counter() - t0)
-    # the same single-update call on the batch engine only (lcv_set_latency_mode(0))
-    prev = getattr(v, "latency_mode", 32)
-    v.set_latency_mode(0)
+    # the same single-update call on the opt-in latency engines (lcv_set_latency_mode(32))
+    prev = getattr(v, "latency_mode", 0)
+    v.set_latency_mode(32)
     try:
         v.validate(one, sb.current_slot, gvr)
         tb = []
@@ -539,11 +539,12 @@ def latency_lines(v, sb, calls: int = 20) -> dict:
     finally:
         v.set_latency_mode(prev)
     return {"validate_one_update_ms": round(1000 * float(np.median(ts)), 3), "validate_one_update_valid": bool(ok[0]),
-            "validate_one_update_batch_engine_ms": round(1000 * float(np.median(tb)), 3),
+            "validate_one_update_latency_engines_ms": round(1000 * float(np.median(tb)), 3),
             "fast_aggregate_verify_512_ms": round(1000 * float(np.median(tf)), 3),
             "fast_aggregate_verify_512_cold_ms": round(1000 * first, 3), "fast_aggregate_verify_valid": bool(fav_ok),
-            "note": "latency engine on (lcv_set_latency_mode(32), default): signature decoding and the SSWU maps "
-                    "one update per wave, products spread over the lanes; *_batch_engine_ms with it off"}
+            "note": "batch engine (default); *_latency_engines_ms with lcv_set_latency_mode(32): signature decoding "
+                    "and the SSWU maps one update per wave (products spread over the lanes), the SOP programs on "
+                    "the quad engine (four lanes per op) - measured slower, off by default (DESIGN.md 3.5)"}
 
 
 def wire_path(v, sb, n: int) -> dict:

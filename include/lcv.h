@@ -150,8 +150,10 @@ int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
 /* Latency engine for small batches (the reference's per-update usage: validate_light_client_update and
  * bls.FastAggregateVerify once per update, sync-protocol.md:512, :464): calls whose batch (or chunk) has
  * at most max_rows rows run signature decoding and the SSWU maps (their Fp exponentiation chains) one
- * item per wave, each Montgomery product spread over the wave's lanes.  Results are identical to the
- * batch engine's.  Default 32; 0 = batch engine always.  Performance knob only. */
+ * item per wave, each Montgomery product spread over the wave's lanes, and the SOP programs (pairing,
+ * hash_to_G2 tail) with four lanes per op.  Results are identical to the batch engine's.  Default 0 (batch
+ * engine always): measured on the MI355X neither engine shortens one update; kept as an
+ * experiment.  Performance knob only. */
 int lcv_set_latency_mode(lcv_ctx* ctx, uint64_t max_rows);
 /* kernel time of the last validate call: total and per stage (ms); names via lcv_stage_name
  * (stage times are recorded by the serial shape only: zero under a multi-stream pipeline) */

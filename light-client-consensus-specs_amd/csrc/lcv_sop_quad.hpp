@@ -45,6 +45,9 @@ LCV_FN void quad_ptable(uint32_t pz[16], uint32_t q) {
       v[s] = (idx >= 1 && idx <= 13) ? kP28.v[idx] : 0u;
     }
     pz[e] = q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+    // opaque 32-bit values from here on: otherwise clang carries the table as 64-bit selects of
+    // constants and emits a 64 x 32-bit multiply (two v_mad_u64_u32 and moves) per column update
+    asm volatile("" : "+v"(pz[e]));
   }
 }
 

@@ -112,7 +112,7 @@ class Verifier:
             raise LcvError(f"lcv_init(device={device}) failed with status {rc}")
         self.device = device
         self.config = _config.MAINNET  # the context's network configuration (lcv_init: mainnet)
-        self.latency_mode = 32  # lcv_set_latency_mode's value (lcv_init's default)
+        self.latency_mode = 0  # lcv_set_latency_mode's value (lcv_init's default: batch engine always)
 
     # ------------------------------------------------------------------ plumbing
     def _check(self, rc: int, what: str):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-stage kernel times (HIP events) of ONE update validated through the C ABI, with the latency engine
-(lcv_set_latency_mode, default) and with the batch engine — where the single-call latency of the
+(lcv_set_latency_mode(32), opt-in) and with the batch engine (the default) — where the single-call latency of the
 reference-shaped drop-in (sync-protocol.md:512 -> :464) goes.  GPU only."""
 import json
 import os

@@ -65,6 +65,9 @@ def main():
     args = ap.parse_args()
     out = count(args.n, args.participation)
     path = os.path.join(ROOT, "profiles", "opcounts.json")
+    if os.path.exists(path):  # keep the sections other tools own (tools/canonical_count.py: "canonical")
+        prev = json.load(open(path))
+        out = {**{k: v for k, v in prev.items() if k not in out}, **out}
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
