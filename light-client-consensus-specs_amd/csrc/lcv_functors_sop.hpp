@@ -194,19 +194,20 @@ struct F_sop_h2c {
 };
 
 #ifdef LCV_KERNEL_UNIT
-// The SOP round loop: one wave per block, 64 / TEAM teams (items) per wave, lanes past the last team
-// idle.  The round header is wave-uniform (scalar loads); each lane reads its record from global
+// The SOP round loop: one wave per block, g <= 64 / TEAM teams (items) per wave, lanes past the last
+// team idle.  The round header is wave-uniform (scalar loads); each lane reads its record from global
 // memory (L2-resident program).  Blocks are one wave, so the barrier between rounds is a wave barrier.
 template <class F>
 // LDS is dynamic (sized at launch): with a static size the compiler derives its occupancy target from
 // a smaller LDS than gfx950's 160 KB and gives the kernel 256 VGPRs (2 waves/SIMD).
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) void k_sop(F f, uint32_t n) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) void k_sop(F f, uint32_t n, uint32_t g) {
   constexpr uint32_t T = F::TEAM, G = 64 / F::TEAM;
+  if (g == 0 || g > G) g = G;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // 16-byte aligned values (LCV_SOP_B128)
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
-  const uint32_t item = blockIdx.x * G + team;
-  const bool active = team < G && item < n;
-  uint32_t* my = lds + F::SHARED_WORDS + (team < G ? team : 0) * F::LDS_WORDS;
+  const uint32_t item = blockIdx.x * g + team;
+  const bool active = team < g && item < n;
+  uint32_t* my = lds + F::SHARED_WORDS + (team < g ? team : 0) * F::LDS_WORDS;
   for (uint32_t k = threadIdx.x; k < F::SHARED_WORDS; k += 64) lds[k] = f.P.consts[k];
   if (active) f.prologue(item, lane, my);
   __syncthreads();

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <new>
 #include <thread>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -236,7 +237,9 @@ template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t 
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n) {
   if (n == 0) return LCV_OK;
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  HIPCHK(ctx, lcv_hip_launch_sop<F>(f, n, cur_stream(ctx)));
+  uint32_t g = 0;  // items per wave: the most that fit, except hash_to_G2's tail under LCV_SOP_H2C_ITEMS
+  if constexpr (std::is_same<F, F_sop_h2c>::value) g = ctx->h2c_items;
+  HIPCHK(ctx, lcv_hip_launch_sop<F>(f, n, cur_stream(ctx), g));
   return LCV_OK;
 }
 

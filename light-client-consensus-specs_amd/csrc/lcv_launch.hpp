@@ -9,7 +9,7 @@
 
 template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t s);
 template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s);
-template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s);
+template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s, uint32_t g = 0);
 template <class F> hipError_t lcv_hip_launch_sop_quad(const F& f, uint32_t n, hipStream_t s);
 // the latency engine (lcv_k_wide.hip): one item per wave, products spread over the lanes
 template <class F> hipError_t lcv_hip_launch_wide(const F& f, uint32_t n, hipStream_t s);
@@ -48,13 +48,15 @@ template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStr
   hipLaunchKernelGGL(k_team<F>, dim3(blocks), dim3(64), 0, s, f, n);
   return hipGetLastError();
 }
-// SOP functors (lcv_functors_sop.hpp): the k_sop round loop, 64 / TEAM items per one-wave block
-template <class F> __global__ void k_sop(F f, uint32_t n);
-template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s) {
+// SOP functors (lcv_functors_sop.hpp): the k_sop round loop, g items per one-wave block (g = 0: the
+// most that fit, 64 / TEAM; fewer items per wave = more waves per SIMD for the same batch)
+template <class F> __global__ void k_sop(F f, uint32_t n, uint32_t g);
+template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s, uint32_t g) {
   constexpr uint32_t G = 64 / F::TEAM;
-  const uint32_t blocks = (n + G - 1) / G;
-  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + G * F::LDS_WORDS);
-  hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), lds_bytes, s, f, n);
+  if (g == 0 || g > G) g = G;
+  const uint32_t blocks = (n + g - 1) / g;
+  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + g * F::LDS_WORDS);
+  hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), lds_bytes, s, f, n, g);
   return hipGetLastError();
 }
 // the quad engine (latency mode, lcv_sop_quad.hpp): one item per one-wave block, 4 lanes per op
@@ -65,7 +67,7 @@ template <class F> hipError_t lcv_hip_launch_sop_quad(const F& f, uint32_t n, hi
   hipLaunchKernelGGL(k_sop_quad<F>, dim3(n), dim3(64), lds_bytes, s, f, n);
   return hipGetLastError();
 }
-#define LCV_INSTANTIATE_SOP(F) template hipError_t lcv_hip_launch_sop<F>(const F&, uint32_t, hipStream_t);
+#define LCV_INSTANTIATE_SOP(F) template hipError_t lcv_hip_launch_sop<F>(const F&, uint32_t, hipStream_t, uint32_t);
 #define LCV_INSTANTIATE_SOP_QUAD(F) template hipError_t lcv_hip_launch_sop_quad<F>(const F&, uint32_t, hipStream_t);
 #define LCV_INSTANTIATE(F) template hipError_t lcv_hip_launch<F>(const F&, uint32_t, hipStream_t);
 #define LCV_INSTANTIATE_TEAM(F) template hipError_t lcv_hip_launch_team<F>(const F&, uint32_t, hipStream_t);

@@ -84,3 +84,22 @@ def test_latency_engine_fast_aggregate_verify(gpu_verifier):
     sig = B.aggregate_signatures([B.sign(k, msg) for k in sks])
     (a, b) = _both(v, lambda: (v.fast_aggregate_verify(pks, msg, sig), v.fast_aggregate_verify(pks, b"\x43" * 32, sig)))
     assert a == b == (True, False)
+
+
+@pytest.mark.parametrize("items", [1, 5, 6])
+def test_h2c_items_per_wave(gpu_verifier, items, monkeypatch):
+    """hash_to_G2's tail with fewer items per wave (LCV_SOP_H2C_ITEMS, read at lcv_init): a ragged batch
+    (37 messages: partial last wave) gives the default launch's points bit for bit, and the oracle's."""
+    import os
+    from lcv.device import Verifier
+    rng = random.Random(60 + items)
+    msgs = np.frombuffer(bytes(rng.randrange(256) for _ in range(32 * 37)), np.uint8)
+    h_ref, i_ref = gpu_verifier.debug_hash_to_g2(msgs)
+    monkeypatch.setenv("LCV_SOP_H2C_ITEMS", str(items))
+    v = H.hostsim_verifier() if os.environ.get("LCV_TEST_HOSTSIM") == "1" else Verifier(0)
+    h, inf = v.debug_hash_to_g2(msgs)
+    assert np.array_equal(h, h_ref) and np.array_equal(inf, i_ref)
+    for i in (0, 36):
+        e = B.hash_to_g2(msgs[32 * i:32 * i + 32].tobytes())
+        got = [int.from_bytes(h[i][48 * k:48 * k + 48].tobytes(), "big") for k in range(4)]
+        assert got == [e[0][0], e[0][1], e[1][0], e[1][1]]
