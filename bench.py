@@ -399,11 +399,15 @@ def main():
             ops = total_ops_per_update(args.n, npool, sec)
             rate = ops * total / dt / world / 1e12
             roof[f"pipeline_ops_per_update_{sec}"] = round(ops, 1)
-            roof[f"pipeline_frac_{sec}"] = round(rate / PEAK_MAC_TOPS, 4)
-            roof[f"pipeline_frac_{sec}_vs_int32_valu_peak"] = round(rate / PEAK_INT32_VALU_TOPS, 4)
-        # headline: the executed numerator; the canonical one beside it charges textbook inversions and
-        # square roots the device does not run (CANONICAL_MATCHED), so it is not a hardware fraction
-        roof["pipeline_frac"] = roof["pipeline_frac_executed"]
+            if sec == "executed":
+                roof["pipeline_frac_executed"] = round(rate / PEAK_MAC_TOPS, 4)
+                roof["pipeline_frac_executed_vs_int32_valu_peak"] = round(rate / PEAK_INT32_VALU_TOPS, 4)
+            else:
+                # the textbook algorithms' op count at the measured update rate: a work-equivalent rate,
+                # NOT a fraction of any peak (it charges Fermat inversions / square roots and a textbook
+                # Miller loop the device does not run, so it can exceed the hardware's rate)
+                roof["pipeline_canonical_equivalent_T_ops_per_s"] = round(rate, 3)
+        roof["pipeline_frac"] = roof["pipeline_frac_executed"]  # headline: the executed numerator
     configs = None if (args.no_configs or args.quick or world > 1) else config_lines(v)
     out = {
         "metric": "verified LightClientUpdates/sec (512-member committee)",
