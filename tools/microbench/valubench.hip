@@ -120,13 +120,58 @@ __global__ __launch_bounds__(64) void k_add64(unsigned long long* cyc, uint64_t*
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// half the waves run the mad loop, half the add loop (by block parity): does a SIMD overlap one wave's
+// back-to-back v_mad_u64_u32 with ANOTHER wave's full-rate instructions (compare with mad and add alone)?
+__global__ __launch_bounds__(64) void k_split(unsigned long long* cyc, uint64_t* out, uint32_t s) {
+  if (blockIdx.x & 1) {
+    uint32_t x[7], y[7];
+    uint64_t c[13];
+    for (int i = 0; i < 7; ++i) { x[i] = (threadIdx.x + s) * 2654435761u + i; y[i] = x[i] ^ 0x9e3779b9u; }
+    for (int i = 0; i < 13; ++i) c[i] = i;
+    const unsigned long long t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) c[i + j] += (uint64_t)x[i] * y[j];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) x[i] ^= (uint32_t)c[i];
+    }
+    const unsigned long long t1 = clock64();
+    uint64_t r = 0;
+    for (int i = 0; i < 13; ++i) r ^= c[i];
+    out[blockIdx.x * 64 + threadIdx.x] = r;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  } else {
+    uint32_t x[7], y[7], d[13];
+    for (int i = 0; i < 7; ++i) { x[i] = (threadIdx.x + s) * 2654435761u + i; y[i] = x[i] ^ 0x9e3779b9u; }
+    for (int i = 0; i < 13; ++i) d[i] = 3 * i;
+    const unsigned long long t0 = clock64();
+    // 2 x 49 + 14 simple ops per iteration, about the mad loop's duration alone
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) d[i + j] += x[j] ^ y[i];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) x[i] ^= d[i];
+    }
+    const unsigned long long t1 = clock64();
+    uint64_t r = 0;
+    for (int i = 0; i < 13; ++i) r ^= d[i];
+    out[blockIdx.x * 64 + threadIdx.x] = r;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  }
+}
+
 typedef void (*kfn)(unsigned long long*, uint64_t*, uint32_t);
 struct K { const char* name; kfn f; };
 
 int main() {
   K ks[] = {{"mad  (49 v_mad_u64_u32 + 7 xor)", k_mad}, {"add  (49 x (add, xor) + 7 xor)", k_add},
             {"mix  (49 mad + 49 x (xor, add) + 14)", k_mix}, {"fma64 (56 v_fma_f64)", k_fma64},
-            {"add64 (49 x 2 u64 shift-add + 7 u64 xor)", k_add64}};
+            {"add64 (49 x 2 u64 shift-add + 7 u64 xor)", k_add64},
+            {"split (odd waves: mad loop; even: xad loop)", k_split}};
   const int Ws[] = {1, 2, 3, 4, 8};
   unsigned long long* dcyc;
   uint64_t* out;
