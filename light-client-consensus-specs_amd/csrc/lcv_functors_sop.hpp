@@ -207,8 +207,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
   const uint32_t team = threadIdx.x / T, lane = threadIdx.x % T;
   const uint32_t item = blockIdx.x * g + team;
   const bool active = team < g && item < n;
-  uint32_t* my = lds + F::SHARED_WORDS + (team < g ? team : 0) * F::LDS_WORDS;
+  // LDS: the program's constants, the q p table of the reductions (lcv::sop_reduce), the items' slots
+  static_assert(lcv::SOP_QP_WORDS == LCV_SOP_QP_WORDS, "k_sop's LDS size (lcv_launch.hpp)");
+  uint32_t* qp = lds + F::SHARED_WORDS;
+  uint32_t* my = qp + lcv::SOP_QP_WORDS + (team < g ? team : 0) * F::LDS_WORDS;
   for (uint32_t k = threadIdx.x; k < F::SHARED_WORDS; k += 64) lds[k] = f.P.consts[k];
+  if (threadIdx.x < lcv::SOP_QP_N) lcv::sop_qp_entry(qp + 16 * threadIdx.x, threadIdx.x);
   if (active) f.prologue(item, lane, my);
   __syncthreads();
   const uint32_t* io_in = active ? f.io_in(item) : nullptr;
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
       wn = f.P.rec + off + lane * words;
       if (active) pre = lcv::sop_pre(h0, wn);
     }
-    if (active) lcv::sop_exec(ch0, ch3, w, cur, my, my, lds, ns, io_in, io_out);
+    if (active) lcv::sop_exec(ch0, ch3, w, cur, my, my, lds, ns, io_in, io_out, qp);
     __syncthreads();
   }
   if (active) f.epilogue(item, lane, my);

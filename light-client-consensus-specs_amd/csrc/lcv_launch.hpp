@@ -48,6 +48,8 @@ template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStr
   hipLaunchKernelGGL(k_team<F>, dim3(blocks), dim3(64), 0, s, f, n);
   return hipGetLastError();
 }
+// the reductions' q p table after the constants (lcv_sop.hpp SOP_QP_WORDS, checked in k_sop)
+#define LCV_SOP_QP_WORDS 128u
 // SOP functors (lcv_functors_sop.hpp): the k_sop round loop, g items per one-wave block (g = 0: the
 // most that fit, 64 / TEAM; fewer items per wave = more waves per SIMD for the same batch)
 template <class F> __global__ void k_sop(F f, uint32_t n, uint32_t g);
@@ -55,7 +57,7 @@ template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStre
   constexpr uint32_t G = 64 / F::TEAM;
   if (g == 0 || g > G) g = G;
   const uint32_t blocks = (n + g - 1) / g;
-  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + g * F::LDS_WORDS);
+  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + LCV_SOP_QP_WORDS + g * F::LDS_WORDS);
   hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), lds_bytes, s, f, n, g);
   return hipGetLastError();
 }
