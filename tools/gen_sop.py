@@ -297,6 +297,28 @@ class Program:
         self.zero = self.base_const + self.consts[0]
         assert self.base_const + len(self.consts) < SLOT_MASK
 
+    def relabel(self, perm):
+        """Renumber the program's slots (perm: old slot -> new slot, a permutation of range(nslots)),
+        after finalize: every op's destination / shadow / side-load slot, add-in and product terms and the
+        named slots move together, so the program computes the same values (tools/bank_model.py picks
+        perm to lower the modelled LDS bank conflicts)."""
+        assert sorted(perm) == list(range(self.nslots))
+
+        def m(s):
+            return perm[s] if isinstance(s, int) and 0 <= s < self.nslots else s
+        for ops in self.rounds:
+            for o in ops:
+                o.dst = None if o.dst is None else m(o.dst)
+                o.dst_shadow = None if o.dst_shadow is None else m(o.dst_shadow)
+                o.load_shadow = None if o.load_shadow is None else m(o.load_shadow)
+                if o.load:
+                    o.load = (m(o.load[0]), o.load[1])
+                o.adds = [(m(a), c) for a, c in o.adds]
+                for x, y, _ in o.prods:  # new term objects: one T may sit in several places
+                    x[:] = [T(m(t.slot), t.neg) for t in x]
+                    y[:] = [T(m(t.slot), t.neg) for t in y]
+        self.named = {k: m(v) for k, v in self.named.items()}
+
     def pterm(self, s):
         """Product-term halfword of slot or constant s: PCONST (constant) | the value's byte offset in its
         LDS table; the device address is lds + offset + (flag ? constants - lds : 0) (lcv_sop.hpp
@@ -1468,7 +1490,15 @@ def build():
     ap = acc_program(nsteps=lp.nsteps)
     fp = fexp_program()
     hp = h2c_program()
-    return lp, ap, fp, hp
+    progs = (lp, ap, fp, hp)
+    perms = os.environ.get("LCV_SOP_SLOT_PERMS")  # experiment: JSON {program: perm}
+    if perms:
+        import json
+        for p, perm in json.load(open(perms)).items():
+            prog = {q.name: q for q in progs}[p]
+            prog.finalize()
+            prog.relabel(perm)
+    return progs
 
 
 def main():
