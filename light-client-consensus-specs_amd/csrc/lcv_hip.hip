@@ -237,8 +237,11 @@ template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t 
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n) {
   if (n == 0) return LCV_OK;
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  uint32_t g = 0;  // items per wave: the most that fit, except hash_to_G2's tail under LCV_SOP_H2C_ITEMS
-  if constexpr (std::is_same<F, F_sop_h2c>::value) g = ctx->h2c_items;
+  uint32_t g = 0;  // items per wave: the most that fit unless LCV_SOP_ITEMS_<PROGRAM> says fewer
+  if constexpr (std::is_same<F, F_sop_lines>::value) g = ctx->sop_items[0];
+  if constexpr (std::is_same<F, F_sop_acc>::value) g = ctx->sop_items[1];
+  if constexpr (std::is_same<F, F_sop_fexp>::value) g = ctx->sop_items[2];
+  if constexpr (std::is_same<F, F_sop_h2c>::value) g = ctx->sop_items[3];
   HIPCHK(ctx, lcv_hip_launch_sop<F>(f, n, cur_stream(ctx), g));
   return LCV_OK;
 }

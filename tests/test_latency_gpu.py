@@ -88,14 +88,14 @@ def test_latency_engine_fast_aggregate_verify(gpu_verifier):
 
 @pytest.mark.parametrize("items", [1, 5, 6])
 def test_h2c_items_per_wave(gpu_verifier, items, monkeypatch):
-    """hash_to_G2's tail with fewer items per wave (LCV_SOP_H2C_ITEMS, read at lcv_init): a ragged batch
+    """hash_to_G2's tail with fewer items per wave (LCV_SOP_ITEMS_H2C, read at lcv_init): a ragged batch
     (37 messages: partial last wave) gives the default launch's points bit for bit, and the oracle's."""
     import os
     from lcv.device import Verifier
     rng = random.Random(60 + items)
     msgs = np.frombuffer(bytes(rng.randrange(256) for _ in range(32 * 37)), np.uint8)
     h_ref, i_ref = gpu_verifier.debug_hash_to_g2(msgs)
-    monkeypatch.setenv("LCV_SOP_H2C_ITEMS", str(items))
+    monkeypatch.setenv("LCV_SOP_ITEMS_H2C", str(items))
     v = H.hostsim_verifier() if os.environ.get("LCV_TEST_HOSTSIM") == "1" else Verifier(0)
     h, inf = v.debug_hash_to_g2(msgs)
     assert np.array_equal(h, h_ref) and np.array_equal(inf, i_ref)
@@ -103,3 +103,22 @@ def test_h2c_items_per_wave(gpu_verifier, items, monkeypatch):
         e = B.hash_to_g2(msgs[32 * i:32 * i + 32].tobytes())
         got = [int.from_bytes(h[i][48 * k:48 * k + 48].tobytes(), "big") for k in range(4)]
         assert got == [e[0][0], e[0][1], e[1][0], e[1][1]]
+
+
+@pytest.mark.parametrize("items", [3, 4])
+def test_pairing_items_per_wave(gpu_verifier, items, monkeypatch):
+    """The pairing's SOP kernels (line walk, Miller accumulation, final exponentiation) with fewer items per
+    wave (LCV_SOP_ITEMS_LINES / _ACC / _FEXP): pairing values of a ragged batch equal the default launch's."""
+    import os
+    from lcv.device import Verifier
+    rng = random.Random(70 + items)
+    ps = [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(7)]
+    qs = [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(7)]
+    p96 = np.frombuffer(b"".join(x.to_bytes(48, "big") + y.to_bytes(48, "big") for x, y in ps), np.uint8)
+    q192 = np.frombuffer(b"".join(q[0][0].to_bytes(48, "big") + q[0][1].to_bytes(48, "big") + q[1][0].to_bytes(48, "big")
+                                  + q[1][1].to_bytes(48, "big") for q in qs), np.uint8)
+    ref = gpu_verifier.debug_pairing(p96, q192)
+    for name in ("LINES", "ACC", "FEXP"):
+        monkeypatch.setenv(f"LCV_SOP_ITEMS_{name}", str(items))
+    v = H.hostsim_verifier() if os.environ.get("LCV_TEST_HOSTSIM") == "1" else Verifier(0)
+    assert np.array_equal(v.debug_pairing(p96, q192), ref)
