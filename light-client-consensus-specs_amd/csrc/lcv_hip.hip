@@ -376,7 +376,9 @@ static int be_comm_wait(lcv_ctx* ctx) { return be_comm_wait_stream(ctx, cur_stre
 static int be_comm_shrink(lcv_ctx* ctx, const int* exclude, int nexclude, int* rank, int* nranks) {
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
   ncclComm_t nc = nullptr;
-  ncclResult_t r = ncclCommShrink(ctx->be.comm, const_cast<int*>(exclude), nexclude, &nc, nullptr, NCCL_SHRINK_ABORT);
+  // a failed parent first has its outstanding operations terminated (NCCL_SHRINK_ABORT)
+  const int flags = ctx->comm_failed ? NCCL_SHRINK_ABORT : NCCL_SHRINK_DEFAULT;
+  ncclResult_t r = ncclCommShrink(ctx->be.comm, const_cast<int*>(exclude), nexclude, &nc, nullptr, flags);
   if (r != ncclSuccess || !nc) return nccl_fail(ctx, r, "ncclCommShrink");
   (void)ncclCommAbort(ctx->be.comm);
   ctx->be.comm = nc;

@@ -167,16 +167,35 @@ class Comm:
         return survivors
 
     def recover(self, grace: float = 10.0) -> list:
-        """Shrink the failed communicator to the surviving ranks (same decision on every survivor);
-        returns the survivors' original rank ids.  Afterwards self.rank / self.world are the new ones."""
+        """Move the survivors of a failed communicator (same decision on every survivor) onto a new one;
+        returns the survivors' original rank ids.  Afterwards self.rank / self.world are the new ones.
+        First ncclCommShrink (lcv_comm_shrink); where the RCCL build refuses it, the failed communicator
+        is aborted and the survivors initialise a fresh one through the rendezvous directory (a key per
+        recovery epoch; the lowest surviving rank publishes the id)."""
         survivors = self.agree_survivors(grace)
         exclude = [k for k, r in enumerate(self.ranks) if r not in survivors]
+        me = self.ranks[self.rank]
         ex = (C.c_int * max(1, len(exclude)))(*exclude)
         nr, nn = C.c_int(), C.c_int()
-        self.v._check(self.v.lib.lcv_comm_shrink(self.v.ctx, ex, len(exclude), C.byref(nr), C.byref(nn)),
-                      "lcv_comm_shrink")
+        rc = -1 if os.environ.get("LCV_TEST_NO_SHRINK") == "1" else \
+            self.v.lib.lcv_comm_shrink(self.v.ctx, ex, len(exclude), C.byref(nr), C.byref(nn))
         self.ranks = [r for r in self.ranks if r in survivors]
-        self.rank, self.world = int(nr.value), int(nn.value)
+        self.last_recovery = "shrink" if rc == 0 else "reinit"
+        if rc not in (0, -1):
+            msg = self.v.lib.lcv_last_error(self.v.ctx)
+            self.last_recovery += f" (lcv_comm_shrink: {msg.decode() if msg else rc})"
+        if rc == 0:
+            self.rank, self.world = int(nr.value), int(nn.value)
+        else:
+            self.v.lib.lcv_comm_abort(self.v.ctx)
+            self.rank, self.world = self.ranks.index(me), len(self.ranks)
+            base = self.key if self.key is not None else \
+                f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}_{os.environ.get('MASTER_PORT', '0')}"
+            key = f"{base}.epoch{self.epoch + 1}"
+            uid = rendezvous(self.v.lib, self.rank, self.world, key)
+            self.v._check(self.v.lib.lcv_comm_init(self.v.ctx, self.world, self.rank, ptr(as_u8(uid))),
+                          "lcv_comm_init (recovery)")
+            self._epoch_keys = getattr(self, "_epoch_keys", []) + [key]
         if self.world != len(self.ranks):
             raise CommFailed(f"shrunk communicator has {self.world} ranks, the survivors' decision {len(self.ranks)}")
         self.epoch += 1
@@ -218,11 +237,12 @@ class Comm:
         if self.v is not None:
             try:
                 self.barrier()
-            except CommFailed:
-                pass  # a failed communicator is aborted by lcv_comm_destroy
+            except LcvError:
+                pass  # a failed (or already aborted) communicator: lcv_comm_destroy aborts / skips it
             if self.rank == 0:
                 import glob
-                for f in [_id_path(self.key)] + glob.glob(f"{_id_path(self.key)}.*.fail*"):
+                keys = [self.key] + getattr(self, "_epoch_keys", [])
+                for f in [_id_path(k) for k in keys] + glob.glob(f"{_id_path(self.key)}.*.fail*"):
                     try:
                         os.remove(f)
                     except OSError:

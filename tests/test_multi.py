@@ -85,11 +85,14 @@ def test_two_rank_gloo():
         assert t == 2.0
 
 
-def _fail_worker(rank, world, dead, port, q):
+def _fail_worker(rank, world, dead, port, q, noshrink=False):
     """Rank `dead` dies before its collective (lcv.multi's LCV_TEST_FAIL_RANK hook); the survivors'
     collective times out (communicator timeout 3 s), they agree on who is left, shrink the communicator
-    and re-validate the batch over themselves."""
+    (or, noshrink: abort it and initialise a fresh one among themselves, the path for RCCL builds that
+    refuse ncclCommShrink) and re-validate the batch over themselves."""
     os.environ["LCV_TEST_FAIL_RANK"] = str(dead)
+    if noshrink:
+        os.environ["LCV_TEST_NO_SHRINK"] = "1"
     from lcv import multi, synth
     v = H.hostsim_verifier()
     kinds = np.array([0, 2, 4, 1, 5, 0, 6, 3, 0, 1, 0])
@@ -104,15 +107,15 @@ def _fail_worker(rank, world, dead, port, q):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,dead", [(2, 1), (4, 2)])
-def test_rank_failure_recovery(world, dead):
+@pytest.mark.parametrize("world,dead,noshrink", [(2, 1, False), (4, 2, False), (4, 1, True)])
+def test_rank_failure_recovery(world, dead, noshrink):
     """SURVEY.md §5 (a GPU failing in a shard -> rerun the shard): with one rank dead mid-batch the
     survivors return, and their verdicts equal the single-rank result."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fail_worker, args=(r, world, dead, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, dead, port, q, noshrink)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=500) for _ in range(world - 1)]

@@ -39,3 +39,28 @@ def test_rccl_one_rank(gpu_verifier):
         assert comm.allreduce_max(3.5) == 3.5
     finally:
         comm.close()
+
+
+def test_rccl_failure_entries_one_rank(gpu_verifier):
+    """The failure-containment path on real RCCL (one rank): a bounded collective wait
+    (lcv_comm_set_timeout), Comm.recover — ncclCommShrink, or where this RCCL refuses it, abort and a
+    fresh communicator through the rendezvous — after which the communicator validates, gathers and
+    reduces again, and ncclCommAbort on teardown (lcv_comm_abort)."""
+    if os.environ.get("LCV_TEST_HOSTSIM") == "1":
+        pytest.skip("RCCL: product library only")
+    from lcv import multi, synth
+    kinds = np.array([0, 2, 0, 5])
+    sb = synth.generate(gpu_verifier, len(kinds), seed=52, kinds=kinds)
+    gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    comm = multi.Comm(gpu_verifier, 1, 0, key=f"gputest_fail_{os.getpid()}", timeout=30.0)
+    try:
+        comm.set_timeout(5.0)
+        assert comm.recover(grace=0.5) == [0]
+        print("recovery path:", comm.last_recovery)
+        assert (comm.rank, comm.world) == (0, 1) and comm.count() == 1
+        full = multi.validate_sharded(gpu_verifier, sb.updates, sb.current_slot, sb.genesis_validators_root, comm)
+        assert list(full) == list(sb.expected_verdict)
+        assert comm.allreduce_max(2.0) == 2.0
+        assert gpu_verifier.lib.lcv_comm_abort(gpu_verifier.ctx) == 0
+    finally:
+        comm.close()
