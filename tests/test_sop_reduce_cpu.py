@@ -1,8 +1,9 @@
 """The SOP engine's final reduction (csrc/lcv_sop.hpp sop_reduce: r < 2^red p -> r mod p), compiled for
 the CPU with g++ and checked against Python integers.  For red >= 2 it estimates q = floor(r / p) in
 FP64 from r's top words, subtracts q p (from the q p table for red <= 3, else by multiply-adds) and
-finishes with one conditional subtraction — correct only if the estimate is never above q and at most
-one below; these cases sit on and around every multiple of p up to 2^red p, where that matters."""
+finishes with one conditional subtraction, skipped when the estimate's fractional part proves it exact —
+correct only if the estimate is never above q, at most one below, and the skip test is sound; these cases
+sit on and around every multiple of p up to 2^red p and around the skip threshold, where that matters."""
 import ctypes
 import os
 import random
@@ -52,6 +53,9 @@ def test_sop_reduce_exact(lib, red):
     for k in range(1, 1 << red):
         vals += [k * P - 1, k * P, k * P + 1, k * P + (1 << 320) - 1, k * P - (1 << 320),
                  k * P + rng.randrange(1 << 64), k * P - rng.randrange(1, 1 << 64)]
+        # around the device's skip threshold (fractional part of the estimate within ~2^-29 of 1)
+        for f in (27, 28, 29, 30, 31, 32, 36):
+            vals += [(k + 1) * P - (P >> f), k * P + (P >> f), (k + 1) * P - (P >> f) - 1]
     vals += [rng.randrange(top) for _ in range(300)]
     for use_table in ((0, 1) if red <= 3 else (0,)):
         for v in vals:
