@@ -237,6 +237,19 @@ int lcv_sign_batch(lcv_ctx* ctx, const uint8_t* sk32, const uint8_t* msg32, uint
 /* field ops on (a, b) < p: out per item = a*b, a+b, a-b, a^-1, sqrt_fp2(a + b u) (2 x 48); ok = sqrt exists */
 /* test hook: rows per validate chunk (multiple of 64, <= 65536; default 65536) */
 int lcv_debug_set_chunk(lcv_ctx* ctx, uint64_t rows);
+/* test hook (host arithmetic only): allocates work-space slots 0 .. nslots-1 for `cap` rows and checks
+ * (1) for slices of `slice` rows, that item j of each slice's work view is item base + j of the slot's
+ * work space in every per-item field, element for element, as the kernels address them, and (2) that the
+ * byte ranges of every field of every slot are pairwise disjoint.  LCV_EINVAL + lcv_last_error names the
+ * first field that fails. */
+int lcv_debug_work_check(lcv_ctx* ctx, uint64_t cap, uint64_t slice, int nslots);
+/* test hook (device backend): hold work-space slot `slot`'s main stream with a kernel that waits for
+ * lcv_debug_release_slots or max_seconds (<= 120), so that a collective behind it cannot complete */
+int lcv_debug_hold_slot(lcv_ctx* ctx, int slot, double max_seconds);
+int lcv_debug_release_slots(lcv_ctx* ctx);
+/* build provenance: a hash of the sources liblcv.so was compiled from (tools/build_id.py: csrc/, include/,
+ * tools/gen_sop.py, the Makefile), NUL-terminated into out (cap >= 17); LCV_EINVAL if cap is too small */
+int lcv_build_id(char* out, uint64_t cap);
 /* test hook: HIP events held by the context's stage-timing pool (bounded under asynchronous calls) */
 int lcv_debug_event_pool(lcv_ctx* ctx, uint64_t* events_out);
 int lcv_debug_fp(lcv_ctx* ctx, const uint8_t* a48, const uint8_t* b48, uint64_t n, uint8_t* out288, uint8_t* ok);

@@ -16,6 +16,7 @@ enum { EV_START = 0, EV_PRE, EV_H2C, EV_SIDE, EV_H2D, EV_COUNT };  // EV_H2D: th
 #define LCV_UNROLL _Pragma("GCC unroll 64")
 #define LCV_NOUNROLL _Pragma("GCC unroll 1")
 #define LCV_GLOBAL_PTR
+#define LCV_HDFN static inline
 #else
 #include <hip/hip_runtime.h>
 #define LCV_FN __device__ __forceinline__
@@ -24,6 +25,7 @@ enum { EV_START = 0, EV_PRE, EV_H2C, EV_SIDE, EV_H2D, EV_COUNT };  // EV_H2D: th
 #define LCV_CMEM static __constant__ const
 #define LCV_UNROLL _Pragma("unroll")
 #define LCV_NOUNROLL _Pragma("unroll 1")
+#define LCV_HDFN __host__ __device__ __forceinline__  // layout arithmetic shared with the host driver
 #endif
 
 // Field multiplication strategy on the device:

@@ -14,6 +14,8 @@
 #endif
 
 enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
+// W.lines: item i's two pairings' line values (pairing k at + k * SOP_LINE_VALS * 12 words)
+LCV_HDFN size_t lines_index(size_t i) { return i * (size_t)SOP_LINE_WORDS; }
 // per-item LDS pitch = 12 * slots + SOP_PITCH_PAD words: 4 keeps every value 16-byte aligned for the
 // b128 LDS accesses (LCV_SOP_B128, lcv_sop.hpp); 1 (odd) staggers the teams' banks for 32-bit accesses
 enum { SOP_PITCH_PAD = LCV_SOP_B128 ? 4 : 1 };
@@ -33,7 +35,7 @@ struct F_sop_lines {
   LCV_HD uint32_t pk(uint32_t t) const { return mode == 0 ? (t & 1u) : (mode == 1 ? 1u : 0u); }
   LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
   LCV_HD uint32_t* io_out(uint32_t t) const {
-    return W.lines + (size_t)upd(t) * SOP_LINE_WORDS + (size_t)pk(t) * SOP_LINE_VALS * 12;
+    return W.lines + lines_index(upd(t)) + (size_t)pk(t) * SOP_LINE_VALS * 12;
   }
   // T = (Qx, Qy, 1), Q affine; (-xP, yP).  An identity Q becomes (G2 generator, P = (0, 0)): constant
   // lines, killed by the final exponentiation (e(P, O) = 1).
@@ -100,7 +102,7 @@ struct F_sop_acc {
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
-  LCV_HD const uint32_t* io_in(uint32_t i) const { return W.lines + (size_t)i * SOP_LINE_WORDS; }
+  LCV_HD const uint32_t* io_in(uint32_t i) const { return W.lines + lines_index(i); }
   LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
   // lane l handles the Fp12 coefficients l, l + TEAM, ... (any team size)
   LCV_HD void prologue(uint32_t, uint32_t lane, uint32_t* lds) const {  // f = 1

@@ -37,7 +37,8 @@ struct Backend {
   int base = 0;                          // work-space slot s uses streams st[2s] (main), st[2s + 1] (side)
   hipEvent_t ev[LCV_SLOTS][EV_COUNT] = {};  // run_bls's ordering events, per slot
   ncclComm_t comm = nullptr;  // RCCL communicator (lcv_comm_init), collectives on st[0]
-  double* comm_scalar = nullptr;
+  double* comm_scalar = nullptr;       // device scalar of lcv_comm_allreduce_max
+  double* comm_host_scalar = nullptr;  // its pinned host staging (copies never block the bounded wait)
 };
 
 static int be_init(lcv_ctx* ctx, int device);
@@ -325,14 +326,20 @@ static int be_comm_init(lcv_ctx* ctx, int nranks, int rank, const uint8_t* id) {
     return nccl_fail(ctx, r, "ncclCommInitRank");
   }
   HIPCHK(ctx, hipMalloc((void**)&ctx->be.comm_scalar, sizeof(double)));
+  HIPCHK(ctx, hipHostMalloc((void**)&ctx->be.comm_host_scalar, sizeof(double), hipHostMallocDefault));
   return LCV_OK;
+}
+static void be_comm_free_scalars(lcv_ctx* ctx) {
+  if (ctx->be.comm_scalar) (void)hipFree(ctx->be.comm_scalar);
+  if (ctx->be.comm_host_scalar) (void)hipHostFree(ctx->be.comm_host_scalar);
+  ctx->be.comm_scalar = nullptr;
+  ctx->be.comm_host_scalar = nullptr;
 }
 static void be_comm_destroy(lcv_ctx* ctx) {
   (void)hipSetDevice(ctx->be.device);
   if (ctx->be.comm) (void)ncclCommDestroy(ctx->be.comm);
-  if (ctx->be.comm_scalar) (void)hipFree(ctx->be.comm_scalar);
   ctx->be.comm = nullptr;
-  ctx->be.comm_scalar = nullptr;
+  be_comm_free_scalars(ctx);
 }
 static int be_comm_allgather(lcv_ctx* ctx, const uint8_t* send, uint8_t* recv, size_t per_rank) {
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
@@ -389,18 +396,53 @@ static int be_comm_shrink(lcv_ctx* ctx, const int* exclude, int nexclude, int* r
 static void be_comm_abort(lcv_ctx* ctx) {
   (void)hipSetDevice(ctx->be.device);
   if (ctx->be.comm) (void)ncclCommAbort(ctx->be.comm);
-  if (ctx->be.comm_scalar) (void)hipFree(ctx->be.comm_scalar);
   ctx->be.comm = nullptr;
-  ctx->be.comm_scalar = nullptr;
+  be_comm_free_scalars(ctx);
 }
 static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
   hipStream_t s = ctx->be.st[0];
-  HIPCHK(ctx, hipMemcpyAsync(ctx->be.comm_scalar, inout, sizeof(double), hipMemcpyHostToDevice, s));
+  // both copies go through pinned memory (DMA, asynchronous to the host), so the host reaches the
+  // bounded wait even when the collective can never complete; the caller's double is written after it
+  // (every earlier call ended with its wait, or failed the communicator, which refuses further calls)
+  *ctx->be.comm_host_scalar = *inout;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->be.comm_scalar, ctx->be.comm_host_scalar, sizeof(double), hipMemcpyHostToDevice, s));
   ncclResult_t r = ncclAllReduce(ctx->be.comm_scalar, ctx->be.comm_scalar, 1, ncclFloat64, ncclMax, ctx->be.comm, s);
   if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllReduce");
-  HIPCHK(ctx, hipMemcpyAsync(inout, ctx->be.comm_scalar, sizeof(double), hipMemcpyDeviceToHost, s));
-  return be_comm_wait_stream(ctx, s);
+  HIPCHK(ctx, hipMemcpyAsync(ctx->be.comm_host_scalar, ctx->be.comm_scalar, sizeof(double), hipMemcpyDeviceToHost, s));
+  LCV_TRY(be_comm_wait_stream(ctx, s));
+  *inout = *ctx->be.comm_host_scalar;
+  return LCV_OK;
+}
+
+// ---- test entries: hold a slot's main stream (a one-wave kernel that spins until the host releases it or
+// `max_seconds` of the device's constant-rate clock pass — every wave reaches the exit), so that a
+// collective enqueued behind it cannot complete: the bounded collective waits must then fail the call
+// within the communicator timeout (tests/test_multi_gpu.py)
+__global__ __launch_bounds__(64) void k_hold(const volatile uint32_t* flag, uint64_t max_ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (*flag == 0u && wall_clock64() - t0 < max_ticks) __builtin_amdgcn_s_sleep(127);
+}
+static uint32_t* g_hold_flag = nullptr;  // pinned, mapped host word
+extern "C" int lcv_debug_hold_slot(lcv_ctx* ctx, int slot, double max_seconds) {
+  if (!ctx || slot < 0 || slot >= LCV_SLOTS || !(max_seconds > 0.0) || max_seconds > 120.0)
+    return fail(ctx, LCV_EINVAL, "lcv_debug_hold_slot: slot 0..7, 0 < max_seconds <= 120");
+  HIPCHK(ctx, hipSetDevice(ctx->be.device));
+  if (!g_hold_flag) HIPCHK(ctx, hipHostMalloc((void**)&g_hold_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  __atomic_store_n(g_hold_flag, 0u, __ATOMIC_SEQ_CST);
+  uint32_t* dflag = nullptr;
+  HIPCHK(ctx, hipHostGetDevicePointer((void**)&dflag, g_hold_flag, 0));
+  int khz = 0;
+  HIPCHK(ctx, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->be.device));
+  const uint64_t ticks = (uint64_t)(max_seconds * 1e3 * (double)(khz > 0 ? khz : 100000));
+  hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, ctx->be.st[2 * slot], (const volatile uint32_t*)dflag, ticks);
+  HIPCHK(ctx, hipGetLastError());
+  return LCV_OK;
+}
+extern "C" int lcv_debug_release_slots(lcv_ctx* ctx) {
+  if (!ctx) return LCV_EINVAL;
+  if (g_hold_flag) __atomic_store_n(g_hold_flag, 1u, __ATOMIC_SEQ_CST);
+  return LCV_OK;
 }
 
 extern "C" int lcv_device_count(int* out) {

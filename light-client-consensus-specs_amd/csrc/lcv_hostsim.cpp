@@ -249,6 +249,12 @@ static int be_comm_allreduce_max(lcv_ctx* ctx, double* inout) {
   return LCV_OK;
 }
 
+// the stream-hold test entries need a device queue (lcv_hip.hip); the host simulation refuses them
+extern "C" int lcv_debug_hold_slot(lcv_ctx* ctx, int, double) {
+  return fail(ctx, LCV_EINVAL, "lcv_debug_hold_slot: device backend only");
+}
+extern "C" int lcv_debug_release_slots(lcv_ctx* ctx) { return ctx ? LCV_OK : LCV_EINVAL; }
+
 extern "C" int lcv_device_count(int* out) {
   if (!out) return LCV_EINVAL;
   *out = 1;

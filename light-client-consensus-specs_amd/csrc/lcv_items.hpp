@@ -87,18 +87,26 @@ struct Work {
 // c0.c2, c1.c0, c1.c1, c1.c2 = g0, g2, g4, g1, g3, g5)
 LCV_FN uint32_t fp12_soa_slot(uint32_t g) { return (g & 1u) ? 3u + (g >> 1) : (g >> 1); }
 
+// ---- element addressing of the Work / batch arrays: every accessor below and the host-side layout
+// check (lcv_debug_work_check, lcv_driver.inc) go through these, so the check sees the kernels' addresses
+// SoA: row `row` of item i of an array with stride cap
+LCV_HDFN size_t soa_index(size_t cap, size_t i, size_t row) { return row * cap + i; }
+// item-major W.f: coefficient s of item i (12 words each, 144 per item)
+LCV_HDFN size_t f12_index(size_t i, uint32_t s) { return (i * 12 + s) * 12; }
+enum : uint32_t { F12_ITEM_WORDS = 144 };
+
 // ---- SoA helpers
 LCV_FN void soa_ld_fp(fp& r, const uint32_t* base, size_t cap, size_t i, size_t slot) {
-  LCV_UNROLL for (int k = 0; k < 12; ++k) r.v[k] = base[(slot * 12 + k) * cap + i];
+  LCV_UNROLL for (int k = 0; k < 12; ++k) r.v[k] = base[soa_index(cap, i, slot * 12 + k)];
 }
 LCV_FN void soa_st_fp(uint32_t* base, size_t cap, size_t i, size_t slot, const fp& a) {
-  LCV_UNROLL for (int k = 0; k < 12; ++k) base[(slot * 12 + k) * cap + i] = a.v[k];
+  LCV_UNROLL for (int k = 0; k < 12; ++k) base[soa_index(cap, i, slot * 12 + k)] = a.v[k];
 }
 // W.f (the Miller loop's output, the final exponentiation's e^3): item-major, the 12 Fp coefficients of
 // item i in the SOP programs' slot order (2 g + c for the w^g coefficient, component c), 48 contiguous
 // bytes each, so a team's lanes move their coefficients as 16-byte accesses of one 576-byte row
 LCV_FN void f12_st_coeff(uint32_t* base, size_t i, uint32_t s, const uint32_t v[12]) {
-  uint32_t* d = base + (i * 12 + s) * 12;
+  uint32_t* d = base + f12_index(i, s);
 #if defined(__HIP_DEVICE_COMPILE__)
   uint4* q = (uint4*)d;
   LCV_UNROLL for (int k = 0; k < 3; ++k) q[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
@@ -107,7 +115,7 @@ LCV_FN void f12_st_coeff(uint32_t* base, size_t i, uint32_t s, const uint32_t v[
 #endif
 }
 LCV_FN void f12_ld_coeff(uint32_t v[12], const uint32_t* base, size_t i, uint32_t s) {
-  const uint32_t* d = base + (i * 12 + s) * 12;
+  const uint32_t* d = base + f12_index(i, s);
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint4* q = (const uint4*)d;
   LCV_UNROLL for (int k = 0; k < 3; ++k) {

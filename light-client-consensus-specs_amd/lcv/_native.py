@@ -68,6 +68,10 @@ SIGNATURES = {
     "lcv_comm_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "lcv_debug_event_pool": (C.c_int, [C.c_void_p, u64p]),
     "lcv_debug_set_chunk": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "lcv_debug_work_check": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int]),
+    "lcv_debug_hold_slot": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    "lcv_debug_release_slots": (C.c_int, [C.c_void_p]),
+    "lcv_build_id": (C.c_int, [C.c_char_p, C.c_uint64]),
     "lcv_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
     "lcv_set_pipeline": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "lcv_set_latency_mode": (C.c_int, [C.c_void_p, C.c_uint64]),
@@ -129,6 +133,13 @@ class Lib:
 
     def __getattr__(self, name):
         return getattr(self.dll, name)
+
+    def build_id(self) -> str:
+        """The source hash compiled into the library (tools/build_id.py at build time)."""
+        buf = C.create_string_buffer(64)
+        if self.dll.lcv_build_id(buf, 64) != 0:
+            raise LcvError("lcv_build_id failed")
+        return buf.value.decode()
 
 
 _lib = None

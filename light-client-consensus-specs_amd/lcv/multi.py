@@ -101,11 +101,20 @@ class CommFailed(LcvError):
 class Comm:
     """The RCCL communicator of one rank (on `verifier`'s device).  `timeout`: every collective completes
     within it or fails with CommFailed (lcv_comm_set_timeout); `recover()` then agrees on the surviving
-    ranks and shrinks the communicator to them (lcv_comm_shrink)."""
+    ranks and moves them onto a new communicator.
 
-    def __init__(self, verifier, world: int, rank: int, key: Optional[str] = None, timeout: float = 60.0):
+    `recovery`: "reinit" (default) aborts the failed communicator and the survivors initialise a fresh one
+    through the rendezvous directory — the path that works on the RCCL the MI355X image ships (2.27
+    refuses ncclCommShrink); "shrink" first tries lcv_comm_shrink (ncclCommShrink with
+    NCCL_SHRINK_ABORT) and falls back to "reinit" when RCCL refuses it."""
+
+    def __init__(self, verifier, world: int, rank: int, key: Optional[str] = None, timeout: float = 60.0,
+                 recovery: str = "reinit"):
+        if recovery not in ("reinit", "shrink"):
+            raise ValueError(f"recovery must be 'reinit' or 'shrink', not {recovery!r}")
         self.v, self.world, self.rank = verifier, int(world), int(rank)
         self.key = key
+        self.recovery = recovery
         self.epoch = 0          # recoveries so far
         self.ranks = list(range(self.world))  # original rank ids of the current members, by new rank
         uid = rendezvous(verifier.lib, self.rank, self.world, key)
@@ -114,6 +123,12 @@ class Comm:
 
     def set_timeout(self, seconds: float) -> None:
         self.v._check(self.v.lib.lcv_comm_set_timeout(self.v.ctx, float(seconds)), "lcv_comm_set_timeout")
+        self.timeout = float(seconds)
+
+    def abort(self) -> None:
+        """Abort this rank's communicator (lcv_comm_abort: outstanding collectives are terminated, the
+        streams drain); the rank takes no further part in collectives until a new communicator."""
+        self.v.lib.lcv_comm_abort(self.v.ctx)
 
     def _coll(self, rc: int, what: str) -> None:
         """Collective status: LCV_EDEVICE (-2) from a collective = the communicator failed."""
@@ -129,7 +144,13 @@ class Comm:
     def agree_survivors(self, grace: float = 10.0) -> list:
         """After a failed collective: every live member announces itself, waits until all members did or
         `grace` seconds passed, and the first to publish a decision (exclusive create) fixes the survivor
-        list everyone then uses; a member left out of the decision (it announced too late) raises."""
+        list everyone then uses; a member left out of the decision (it announced too late) aborts its
+        communicator — so none of its streams stays behind the failed collective — and raises.
+
+        The grace period is at least the communicator timeout: survivors detect the failure when their
+        own collective times out, which starts when each enters its wait, so a slower survivor announces
+        up to one timeout after the first."""
+        grace = max(float(grace), getattr(self, "timeout", 0.0))
         me = self.ranks[self.rank]
         open(self._fail_path(f"alive.{me}"), "w").close()
         t0 = time.monotonic()
@@ -163,22 +184,25 @@ class Comm:
             time.sleep(0.01)
         survivors = [int(x) for x in txt.split(",")]
         if me not in survivors:
+            self.abort()
             raise CommFailed(f"rank {me} was excluded by the survivors' decision {survivors}")
         return survivors
 
     def recover(self, grace: float = 10.0) -> list:
         """Move the survivors of a failed communicator (same decision on every survivor) onto a new one;
         returns the survivors' original rank ids.  Afterwards self.rank / self.world are the new ones.
-        First ncclCommShrink (lcv_comm_shrink); where the RCCL build refuses it, the failed communicator
-        is aborted and the survivors initialise a fresh one through the rendezvous directory (a key per
-        recovery epoch; the lowest surviving rank publishes the id)."""
+        recovery "reinit" (the default): the failed communicator is aborted and the survivors initialise
+        a fresh one through the rendezvous directory (a key per recovery epoch; the lowest surviving rank
+        publishes the id).  recovery "shrink": ncclCommShrink (lcv_comm_shrink) first, "reinit" where the
+        RCCL build refuses it."""
         survivors = self.agree_survivors(grace)
         exclude = [k for k, r in enumerate(self.ranks) if r not in survivors]
         me = self.ranks[self.rank]
         ex = (C.c_int * max(1, len(exclude)))(*exclude)
         nr, nn = C.c_int(), C.c_int()
-        rc = -1 if os.environ.get("LCV_TEST_NO_SHRINK") == "1" else \
-            self.v.lib.lcv_comm_shrink(self.v.ctx, ex, len(exclude), C.byref(nr), C.byref(nn))
+        rc = -1
+        if self.recovery == "shrink":
+            rc = self.v.lib.lcv_comm_shrink(self.v.ctx, ex, len(exclude), C.byref(nr), C.byref(nn))
         self.ranks = [r for r in self.ranks if r in survivors]
         self.last_recovery = "shrink" if rc == 0 else "reinit"
         if rc not in (0, -1):
@@ -187,7 +211,7 @@ class Comm:
         if rc == 0:
             self.rank, self.world = int(nr.value), int(nn.value)
         else:
-            self.v.lib.lcv_comm_abort(self.v.ctx)
+            self.abort()
             self.rank, self.world = self.ranks.index(me), len(self.ranks)
             base = self.key if self.key is not None else \
                 f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}_{os.environ.get('MASTER_PORT', '0')}"
@@ -273,8 +297,6 @@ def validate_sharded(verifier, batch, current_slot: int, genesis_validators_root
         world, rank = comm.world, comm.rank
         lo, hi = shard_bounds(batch.n, world, rank)
         per = -(-batch.n // world)
-        if os.environ.get("LCV_TEST_FAIL_RANK") == str(comm.ranks[rank]) and comm.epoch == 0:
-            os._exit(17)  # test hook (tests/test_multi.py): this rank dies before its collective
         if hi > lo:
             rb = verifier.upload(batch.slice(lo, hi))
         else:  # an empty shard still joins the collective (a one-row dummy batch, verdict overwritten)

@@ -58,3 +58,29 @@ def test_no_gpu_fails_loudly():
     from lcv.device import Verifier
     with pytest.raises((LcvError, LcvUnavailable)):
         Verifier(0)
+
+
+def test_build_id_matches_sources():
+    """lcv_build_id: the libraries carry the hash of the sources they were built from (tools/build_id.py),
+    the check __graft_entry__.smoke() runs on the GPU box against the pushed tree."""
+    sys_path = os.path.join(H.ROOT, "tools")
+    import sys
+    if sys_path not in sys.path:
+        sys.path.insert(0, sys_path)
+    from build_id import build_id
+    from lcv._native import Lib
+    assert Lib(H.ensure_hostsim()).build_id() == build_id()
+    if os.path.exists(H.PRODUCT):
+        assert Lib(H.PRODUCT).build_id() == build_id()
+
+
+def test_work_views_alias_nothing():
+    """Work-space aliasing: for every Work field, item j of each slice's work view is
+    item base + j of the slot's work space, element for element, as the kernels address them
+    (lcv_items.hpp soa_index / f12_index, lcv_functors_sop.hpp lines_index), and no two fields of any of
+    the eight slots overlap.  db0f6f9's work_view (W.f, item-major, advanced by `base` instead of
+    base * 144) fails check (1) at the first slice with base > 0: field "f"."""
+    v = H.hostsim_verifier()
+    for cap, slice_, slots in ((4096, 64, 8), (1000, 128, 3), (65536, 4096, 2), (64, 64, 1)):
+        rc = v.lib.lcv_debug_work_check(v.ctx, cap, slice_, slots)
+        assert rc == 0, v.lib.lcv_last_error(v.ctx)

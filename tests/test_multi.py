@@ -85,46 +85,74 @@ def test_two_rank_gloo():
         assert t == 2.0
 
 
-def _fail_worker(rank, world, dead, port, q, noshrink=False):
-    """Rank `dead` dies before its collective (lcv.multi's LCV_TEST_FAIL_RANK hook); the survivors'
-    collective times out (communicator timeout 3 s), they agree on who is left, shrink the communicator
-    (or, noshrink: abort it and initialise a fresh one among themselves, the path for RCCL builds that
-    refuse ncclCommShrink) and re-validate the batch over themselves."""
-    os.environ["LCV_TEST_FAIL_RANK"] = str(dead)
-    if noshrink:
-        os.environ["LCV_TEST_NO_SHRINK"] = "1"
+def _inject_failure(multi, dead, mode):
+    """Failure injection for the worker of original rank `dead` (a monkeypatch inside that process, so
+    the product code carries no test hook): at its first collective (recovery epoch 0) the rank exits
+    ("exit", status 17) or stops itself with SIGSTOP ("hang": it stays alive, holds its files and never
+    answers, so the survivors' bounded wait is what fires)."""
+    import signal
+    orig = multi.Comm.validate_sharded
+
+    def validate_sharded(self, *a, **k):
+        if self.ranks[self.rank] == dead and self.epoch == 0:
+            if mode == "exit":
+                os._exit(17)
+            os.kill(os.getpid(), signal.SIGSTOP)
+        return orig(self, *a, **k)
+
+    multi.Comm.validate_sharded = validate_sharded
+
+
+def _fail_worker(rank, world, dead, port, q, recovery="reinit", mode="exit"):
+    """Rank `dead` dies (or hangs) before its collective; the survivors' collective times out
+    (communicator timeout 3 s), they agree on who is left and move onto a new communicator — recovery
+    "reinit" (abort + a fresh communicator among themselves, the path RCCL 2.27 takes) or "shrink" — and
+    re-validate the batch over themselves."""
     from lcv import multi, synth
+    _inject_failure(multi, dead, mode)
     v = H.hostsim_verifier()
     kinds = np.array([0, 2, 4, 1, 5, 0, 6, 3, 0, 1, 0])
     sb = synth.generate(v, len(kinds), seed=33, kinds=kinds)
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
-    comm = multi.Comm(v, world, rank, key=f"fail_{port}", timeout=3.0)
+    comm = multi.Comm(v, world, rank, key=f"fail_{port}", timeout=3.0, recovery=recovery)
     full = multi.validate_sharded(v, sb.updates, sb.current_slot, sb.genesis_validators_root, comm, grace=3.0)
     single, _ = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
-    t = comm.allreduce_max(float(rank + 1))  # the shrunk communicator keeps working
-    q.put((rank, full.tolist(), single.astype(bool).tolist(), sb.expected_verdict.tolist(), comm.world, comm.ranks, t))
+    t = comm.allreduce_max(float(rank + 1))  # the new communicator keeps working
+    q.put((rank, full.tolist(), single.astype(bool).tolist(), sb.expected_verdict.tolist(), comm.world, comm.ranks, t,
+           comm.last_recovery))
     comm.close()
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,dead,noshrink", [(2, 1, False), (4, 2, False), (4, 1, True)])
-def test_rank_failure_recovery(world, dead, noshrink):
-    """SURVEY.md §5 (a GPU failing in a shard -> rerun the shard): with one rank dead mid-batch the
-    survivors return, and their verdicts equal the single-rank result."""
+@pytest.mark.parametrize("world,dead,recovery,mode", [(2, 1, "reinit", "exit"), (4, 2, "reinit", "exit"),
+                                                      (4, 1, "shrink", "exit"), (3, 1, "reinit", "hang")])
+def test_rank_failure_recovery(world, dead, recovery, mode):
+    """SURVEY.md §5 (a GPU failing in a shard -> rerun the shard): with one rank dead — or hung, stopped
+    by SIGSTOP, so that only the bounded collective wait can notice it — mid-batch the survivors return,
+    and their verdicts equal the single-rank result."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fail_worker, args=(r, world, dead, port, q, noshrink)) for r in range(world)]
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, dead, port, q, recovery, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=500) for _ in range(world - 1)]
-    for r, p in enumerate(procs):
-        p.join(120)
-        assert p.exitcode == (17 if r == dead else 0), (r, p.exitcode)
+    try:
+        res = [q.get(timeout=500) for _ in range(world - 1)]
+        for r, p in enumerate(procs):
+            if r == dead and mode == "hang":
+                continue
+            p.join(120)
+            assert p.exitcode == (17 if r == dead else 0), (r, p.exitcode)
+    finally:
+        for p in procs:  # the stopped rank (and anything left after a failure) is killed by its own handle
+            if p.is_alive():
+                p.kill()
+                p.join(30)
     survivors = [r for r in range(world) if r != dead]
     assert sorted(x[0] for x in res) == survivors
-    for rank, full, single, exp, w, ranks, t in res:
+    for rank, full, single, exp, w, ranks, t, how in res:
         assert full == single == exp
         assert w == world - 1 and ranks == survivors
         assert t == float(max(survivors) + 1)  # the all-reduce over the survivors (original rank + 1)
+        assert how.startswith(recovery)

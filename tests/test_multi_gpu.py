@@ -52,11 +52,15 @@ def test_rccl_failure_entries_one_rank(gpu_verifier):
     kinds = np.array([0, 2, 0, 5])
     sb = synth.generate(gpu_verifier, len(kinds), seed=52, kinds=kinds)
     gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
-    comm = multi.Comm(gpu_verifier, 1, 0, key=f"gputest_fail_{os.getpid()}", timeout=30.0)
+    comm = multi.Comm(gpu_verifier, 1, 0, key=f"gputest_fail_{os.getpid()}", timeout=30.0, recovery="shrink")
     try:
         comm.set_timeout(5.0)
         assert comm.recover(grace=0.5) == [0]
         print("recovery path:", comm.last_recovery)
+        assert (comm.rank, comm.world) == (0, 1) and comm.count() == 1
+        # the default path (abort + a fresh communicator), as RCCL 2.27 needs it
+        comm.recovery = "reinit"
+        assert comm.recover(grace=0.5) == [0] and comm.last_recovery == "reinit"
         assert (comm.rank, comm.world) == (0, 1) and comm.count() == 1
         full = multi.validate_sharded(gpu_verifier, sb.updates, sb.current_slot, sb.genesis_validators_root, comm)
         assert list(full) == list(sb.expected_verdict)
@@ -64,3 +68,37 @@ def test_rccl_failure_entries_one_rank(gpu_verifier):
         assert gpu_verifier.lib.lcv_comm_abort(gpu_verifier.ctx) == 0
     finally:
         comm.close()
+
+
+def test_collective_behind_held_stream_fails_within_timeout(gpu_verifier):
+    """a collective that cannot complete must fail the call within the communicator
+    timeout — the bounded wait comes before any copy into the caller's pageable memory, which would block
+    the host until the stream reached it.  The slot's main stream is held by a spinning one-wave kernel
+    (lcv_debug_hold_slot: it exits when released or after 20 s), so the all-gather and the all-reduce
+    behind it cannot complete: each call must raise CommFailed in about the 2 s timeout, not return after
+    the hold."""
+    if os.environ.get("LCV_TEST_HOSTSIM") == "1":
+        pytest.skip("device streams: product library only")
+    import time
+    from lcv import multi
+    v = gpu_verifier
+    for what in ("slot_allgather", "allreduce_max"):
+        comm = multi.Comm(v, 1, 0, key=f"gputest_hold_{what}_{os.getpid()}", timeout=2.0)
+        try:
+            assert v.lib.lcv_debug_hold_slot(v.ctx, 0, 20.0) == 0
+            t0 = time.monotonic()
+            try:
+                with pytest.raises(multi.CommFailed):
+                    if what == "slot_allgather":
+                        comm.slot_allgather(0, 0, 64)
+                    else:
+                        comm.allreduce_max(1.0)
+                dt = time.monotonic() - t0
+            finally:
+                v.lib.lcv_debug_release_slots(v.ctx)
+            assert dt < 10.0, dt
+            comm.abort()
+        finally:
+            v.lib.lcv_debug_release_slots(v.ctx)
+            comm.close()
+        v.slot_wait(0, 0)  # the held stream has drained (its kernel released, the collective done)
