@@ -39,10 +39,36 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
 
 # Roofline denominators.  The op model W = 600 N_fpmul + 24 N_fpadd +
 # 2100 N_sha prices a Montgomery product at 600 INT32 ops, i.e. 2 ops per multiply-add
-# of a 288-mad product, so its natural peak is the chip's multiply-add issue rate:
-PEAK_MAC_TOPS = 39.3     # 2 ops x v_mad_u64_u32 lane rate: 256 CU x 4 SIMD x 64 lanes / 8 cycles x 2.4 GHz x 2
-# the full-rate INT32 VALU lane rate (4 x SIMD-32 per CU, MI355X_MICROARCH.md; 71.5 T measured by
-# tools/microbench/intbench.hip): every fraction is also reported against it
+# of a 288-mad product, so its natural peak is the chip's multiply-add issue rate, MEASURED: the
+# v_mad_u64_u32 rate of tools/microbench/peakbench.hip (inline asm, 128 independent mads per iteration,
+# no other instruction; wall time over the whole chip) at the SOP kernels' residency of 3 waves per SIMD,
+# committed in profiles/r05_cal/peakbench.txt, x 2 ops per mad.
+PEAK_FILE = os.path.join(ROOT, "profiles", "r05_cal", "peakbench.txt")
+PEAK_WAVES_PER_SIMD = 3
+
+
+def measured_peaks(path: str = PEAK_FILE) -> dict:
+    """Rows of the committed peakbench output: {(kernel, W): {"ms", "ginstr", "cyc_clock", "cyc_24",
+    "mad_T", "op_T"}}."""
+    rows = {}
+    for line in open(path):
+        if line.startswith("#") or "|" not in line:
+            continue
+        head, *cols = [c.strip() for c in line.split("|")]
+        name, w = head.rsplit(None, 1)
+        vals = [float(c) for c in cols]
+        rows[(name.split()[0], int(w))] = dict(zip(("ms", "ginstr", "cyc_clock", "cyc_24", "mad_T", "op_T"), vals))
+    return rows
+
+
+def mac_peak_tops(w: int = PEAK_WAVES_PER_SIMD) -> float:
+    """2 ops x the measured v_mad_u64_u32 rate (T/s) at w waves per SIMD (profiles/r05_cal/peakbench.txt)."""
+    return measured_peaks()[("mad", w)]["op_T"]
+
+
+PEAK_MAC_TOPS = mac_peak_tops()
+# the full-rate INT32 VALU lane rate (4 x SIMD-32 per CU x 2 ops per multiply-add, MI355X_MICROARCH.md):
+# every fraction is also reported against it
 PEAK_INT32_VALU_TOPS = 78.6
 # stages whose canonical (textbook) numerator counts the algorithm class the device runs; elsewhere the
 # canonical counter charges Fermat inversions / square-root chains / a separate psi check the device does
@@ -409,6 +435,7 @@ def main():
                 roof["pipeline_canonical_equivalent_T_ops_per_s"] = round(rate, 3)
         roof["pipeline_frac"] = roof["pipeline_frac_executed"]  # headline: the executed numerator
     configs = None if (args.no_configs or args.quick or world > 1) else config_lines(v)
+    distinct = (configs or {}).get("configs[3]", {}).get("updates_per_s")
     out = {
         "metric": "verified LightClientUpdates/sec (512-member committee)",
         "value": round(total / dt, 1),
@@ -423,8 +450,15 @@ def main():
         "dtype": "u32 (381-bit Montgomery Fp on 12x32-bit limbs; SHA-256 words)",
         "data": "synthetic (mainnet preset, Deneb, device-signed)",
         "config": {"workload": f"configs[1]: {args.n} updates/GPU, {args.participation} participation, "
-                               f"next_sync_committee + finality + execution branches",
+                               f"next_sync_committee + finality + execution branches; the {args.n} updates of a "
+                               f"batch share ONE next_sync_committee value ({npool} distinct per batch, so "
+                               f"HTR(SyncCommittee) runs {npool}x per batch; configs[3] with a distinct committee "
+                               f"per update: value_distinct_committees)",
                    "updates_per_gpu": args.n, "committee": 512, "parallelism": f"dp{world} (independent updates)"},
+        # SURVEY 8(d)'s timed region from host buffers (H2D of the packed batch + kernels + verdicts D2H),
+        # the same serving loop: beside `value`, which the bench contract defines on HBM-resident inputs
+        "value_h2d_inclusive": serving["updates_per_s"],
+        "value_distinct_committees": distinct,
         "all_valid": ok_all and serial_ok,
         "pipeline": {"streams": pipe[0], "slices": pipe[1]},
         "batches_in_flight": args.depth,
@@ -435,7 +469,8 @@ def main():
         # stream beside the message chain, so their sum exceeds the wall time of a step
         "stage_kernel_ms_per_step": stage_avg,
         "sum_of_stage_kernel_ms": round(kernel_ms, 3),
-        "value_is": ("kernel-only: inputs resident in HBM (uploaded once); " +
+        "value_is": ("inputs resident in HBM when the timed region starts (the bench contract); every kernel, "
+                     "the verdict read-back and (N > 1) the RCCL all-gather are inside it; " +
                      (f"{D} batches in flight (serving loop over {D} work-space slots, "
                       "lcv_validate_resident_async): later batches' stages overlap earlier ones', every batch's "
                       "verdicts are waited for and copied out (all-gathered over RCCL for N > 1) inside the "
@@ -457,6 +492,10 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         except Exception as e:  # reported, never fatal to the GPU measurement
             out["cpu_baseline"] = {"error": repr(e)}
+        pc = out["cpu_baseline"].get("per_core_value") if isinstance(out["cpu_baseline"], dict) else None
+        if pc and isinstance(latency, dict) and "validate_one_update_ms" in latency:
+            # the reference's call shape (one update per call) on one CPU core of the same host, beside the GPU's
+            latency["cpu_one_core_ms"] = round(1000.0 / pc, 3)
     print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
@@ -616,10 +655,15 @@ def stage_pmc(stage: str):
 
 
 def pmc_pipe(stage: str):
-    """The VALU-pipe block of the stage's kernel from the committed PMC summary (tools/valu_model.py,
-    tools/pmc_summary.py): cycles its instruction stream needs / the SIMD cycles of the launch."""
+    """The VALU-pipe block of the stage's kernel: the committed PMC counters (tools/pmc_summary.py) priced
+    by tools/valu_model.py with the peakbench cycle costs (the same measurement as the roofline peak):
+    the SIMD cycles its instruction stream needs / the SIMD cycles of the launch."""
     pmc = stage_pmc(stage)
-    return (pmc or {}).get("valu_pipe")
+    if not pmc or "raw" not in pmc:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import valu_model
+    return valu_model.pipe(STAGE_KERNELS[stage], pmc["raw"])
 
 
 def roofline(stage_ms: dict, n: int, npool: int = 1):
@@ -671,9 +715,9 @@ def roofline(stage_ms: dict, n: int, npool: int = 1):
             # counter-only (the profiled launch's instructions x measured cycles / its GRBM cycles), and
             # live: the same cycle need over this run's event time at the nominal 2.4 GHz (the DVFS clock
             # is lower under load, so the live figure understates)
-            d["valu_issue_fraction"] = pp["issue_fraction"]
-            d["valu_pipe_utilization_upper"] = pp["pipe_utilization_upper"]
-            d["valu_issue_fraction_live_2p4ghz"] = round(pp["pipe_cycles_per_launch"] / (sec * 2.4e9 * 1024), 4)
+            d["valu_pipe_busy"] = pp["issue_fraction"]
+            d["mad_share_of_pipe_cycles"] = pp["mad_share_of_pipe_cycles"]
+            d["valu_pipe_busy_live_2p4ghz"] = round(pp["pipe_cycles_per_launch"] / (sec * 2.4e9 * 1024), 4)
         return d
     per = {k: one(k) for k in stage_ms if one(k) is not None}
     if not per:
@@ -686,21 +730,24 @@ def roofline(stage_ms: dict, n: int, npool: int = 1):
     return {"bound": "valu", "kernel": STAGE_KERNELS.get(stage, stage), "stage": stage,
             "achieved": d["achieved"], "peak": PEAK_MAC_TOPS, "unit": "T INT32 op/s", "frac": d["frac"],
             "numerator": "executed (the device's own operations, op model W of SURVEY.md 8(d))",
-            "peak_is": "multiply-add issue peak: 2 ops x v_mad_u64_u32 at quarter rate "
-                       "(256 CU x 4 SIMD x 64 lanes / 8 cycles x 2.4 GHz = 19.66 T mad/s; 19.65 measured)",
+            "peak_is": (f"measured multiply-add issue peak: 2 ops x the v_mad_u64_u32 rate of an all-mad stream "
+                        f"(tools/microbench/peakbench.hip, inline asm, wall time over all 1,024 SIMDs) at "
+                        f"{PEAK_WAVES_PER_SIMD} waves/SIMD, profiles/r05_cal/peakbench.txt"),
+            "peak_by_waves_per_simd": {w: measured_peaks()[("mad", w)]["op_T"] for w in (1, 2, 3, 4, 8)},
             "peak_int32_valu": PEAK_INT32_VALU_TOPS, "frac_vs_int32_valu_peak": d["frac_vs_int32_valu_peak"],
             "frac_canonical": d.get("frac_canonical"),
-            "valu_issue_fraction": d.get("valu_issue_fraction"),
-            "valu_pipe_utilization_upper": d.get("valu_pipe_utilization_upper"),
-            "valu_issue_fraction_live_2p4ghz": d.get("valu_issue_fraction_live_2p4ghz"),
-            "valu_pipe": pmc.get("valu_pipe"),
-            "valu_pipe_is": "rocprofv3 SQ_INSTS_VALU x 4 cycles (+2 per back-to-back v_mad_u64_u32 for the upper "
-                            "bound) over the launch's SIMD cycles (GRBM_GUI_ACTIVE / 8 x 1024); cycles per "
-                            "instruction measured by tools/microbench/valubench.hip (tools/valu_model.py)",
+            "valu_pipe_busy": d.get("valu_pipe_busy"),
+            "mad_share_of_pipe_cycles": d.get("mad_share_of_pipe_cycles"),
+            "valu_pipe_busy_live_2p4ghz": d.get("valu_pipe_busy_live_2p4ghz"),
+            "valu_pipe": pmc_pipe(stage),
+            "valu_pipe_is": "the launch's VALU instructions priced by class (v_mad_u64_u32 C_MAD, other 64-bit "
+                            "C_64, 32-bit C_32: peakbench cycles at 3 waves/SIMD, tools/valu_model.py) over its "
+                            "SIMD cycles (GRBM_GUI_ACTIVE / 8 x 1024); rocprofv3 counters of profiles/pmc_latest.json",
+            "instruction_classes": "profiles/r05_iclass/iclass.md (tools/sop_iclass.py)",
             "valu_busy_pmc": pmc.get("valu_busy"),
             "valu_busy_pmc_is": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: one quad-cycle per VALU instruction "
                                 "issued, whatever its rate (a quarter-rate v_mad_u64_u32 counts once): an issue "
-                                "count per wave, not the pipe's occupancy (valu_issue_fraction)",
+                                "count per wave, not the pipe's occupancy (valu_pipe_busy)",
             "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_unit": "B per launch (rocprofv3 PMC)",
             "ops_per_update_executed": d["ops_executed_per_unit"],
             "ops_per_update_canonical": d.get("ops_canonical_per_unit"),

@@ -9,6 +9,16 @@
 #include "lcv_common.hpp"
 #include "lcv_consts.inc"
 
+// Instruction-class accounting (tools/sop_iclass.py): with -DLCV_SOP_MARKERS the device build places an
+// assembler comment at the start of each region of an SOP round (operands, conversion, MACs, join,
+// reduction, tail steps: lcv_sop.hpp), so the compiled kernel's instructions can be attributed to them.
+// Never set in the product build (a comment-only inline asm still constrains the scheduler).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(LCV_SOP_MARKERS)
+#define SOP_MARK(name) asm volatile("; sopmark " name)
+#else
+#define SOP_MARK(name) ((void)0)
+#endif
+
 namespace lcv {
 
 enum : uint32_t { SOP_M28 = 0x0FFFFFFFu };
@@ -85,6 +95,7 @@ LCV_FN void sop_mac7s(int64_t c[13], const int32_t* x, const int32_t* y) {
 }
 template <bool FIRST>
 LCV_FN void sop_kara_mac(uint64_t p0[13], uint64_t p2[13], int64_t pd[13], const uint32_t x[15], const uint32_t y[14]) {
+  SOP_MARK("kara");
   int32_t xd[7], yd[7];
   LCV_UNROLL for (int i = 0; i < 7; ++i) { xd[i] = (int32_t)(x[i] - x[i + 7]); yd[i] = (int32_t)(y[i + 7] - y[i]); }
   sop_mac7<FIRST>(p0, x, y);
@@ -116,6 +127,7 @@ LCV_FN void sop_redc28(uint32_t r[13], uint64_t col[28]) {
   LCV_UNROLL for (int j = 1; j < 14; ++j) col[13 + j] += (uint64_t)q * kP28.v[j];
   // columns 13..27 -> 28-bit limbs L (L[0] = bits 0..27 of column 13, whose low 20 bits are 0), then
   // word k of the result is bits 20 + 32 k .. 51 + 32 k of the limb string
+  SOP_MARK("normalise");
   uint32_t L[16];
   L[0] = (uint32_t)v & SOP_M28;
   carry = v >> 28;
@@ -125,6 +137,7 @@ LCV_FN void sop_redc28(uint32_t r[13], uint64_t col[28]) {
     carry = t >> 28;
   }
   L[15] = (uint32_t)carry;
+  SOP_MARK("pack");
   LCV_UNROLL for (int k = 0; k < 13; ++k) {
     const int b = 20 + 32 * k, j = b / 28, s = b % 28;
     uint32_t x = L[j] >> s;

@@ -85,6 +85,9 @@ def test_collective_behind_held_stream_fails_within_timeout(gpu_verifier):
     for what in ("slot_allgather", "allreduce_max"):
         comm = multi.Comm(v, 1, 0, key=f"gputest_hold_{what}_{os.getpid()}", timeout=2.0)
         try:
+            # the same call once unheld first: it sizes the communication buffer (growing it later would
+            # free the old one, which waits for every stream, the held one included)
+            assert comm.slot_allgather(0, 0, 64).shape == (64,) and comm.allreduce_max(1.0) == 1.0
             assert v.lib.lcv_debug_hold_slot(v.ctx, 0, 20.0) == 0
             t0 = time.monotonic()
             try:

@@ -91,7 +91,7 @@ def main(src, dst, latest=None):
         if k.startswith("k_sop") or k in ("k_items<F_h2c_map>", "k_items<F_sig>"):
             print(k, {x: d.get(x) for x in ("hbm_bytes_per_launch", "valu_busy", "issue_busy",
                                               "mean_waves_per_simd", "lds_bank_conflict_rate", "valu_insts_per_wave")},
-                  (d.get("valu_pipe") or {}).get("issue_fraction"), (d.get("valu_pipe") or {}).get("pipe_utilization_upper"))
+                  (d.get("valu_pipe") or {}).get("issue_fraction"), (d.get("valu_pipe") or {}).get("mad_share_of_pipe_cycles"))
 
 
 if __name__ == "__main__":

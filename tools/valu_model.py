@@ -3,18 +3,18 @@
 and what fraction of the kernel's SIMD cycles that is — the hardware statement beside the INT32-op
 roofline (bench.py "valu_pipe").
 
-Measured on the box (tools/microbench/valubench.hip, profiles/r04_cal/valubench.txt; shader-clock cycles
-per loop iteration, W >= 2 waves per SIMD):
-  * a wave64 32-bit VALU instruction issues every ~4 SIMD cycles (69 simple ops: 296-306 cycles; the
-    intbench "71.5 T v_add_u32" of round 2 counted an add + xor that the compiler fuses into one
-    v_xad_u32: 35.8 T instructions x 64 lanes, i.e. 4.4 cycles) — 39.3 T lane-instructions/s at 2.4 GHz;
-  * a v_mad_u64_u32 takes ~6 cycles back to back (49 mads + 7 xors: 306 cycles) and ~4 when other
-    instructions sit between mads (49 mads + 84 simple ops: 543 cycles = 133 x 4.08);
-  * v_fma_f64 4.15 cycles; a 64-bit shift-add (v_lshl_add_u64) ~4-5.
-So for a launch with N_valu VALU and N_mad multiply-add wave-instructions (rocprofv3 SQ_INSTS_VALU; N_mad
-exact from the SOP programs, below):
-    issue fraction   = C_VALU * N_valu / S                        (every instruction at 4 cycles)
-    pipe upper bound = (C_VALU * N_valu + (C_MAD - C_VALU) * N_mad) / S   (every mad back to back)
+Cycle costs: ONE source, tools/microbench/peakbench.hip (profiles/r05_cal/peakbench.txt; inline asm, 128
+independent instructions of one kind per loop iteration, wall time over all 1,024 SIMDs at 2.4 GHz), at
+the SOP kernels' residency of 3 waves per SIMD — the same measurement bench.py's roofline peak is:
+  * v_mad_u64_u32 / v_mad_i64_i32: 4.80 / 4.73 SIMD cycles per wave64 instruction (C_MAD);
+  * 64-bit adds (v_lshl_add_u64), v_mul_lo_u32, v_fma_f64: 4.3-4.4 (C_64);
+  * a full-rate 32-bit instruction (v_add_u32): 2.3-3.0 over W = 2..8 (C_32, the median 2.5);
+  * a stream alternating mads and adds (mix) costs the SUM of its parts (4.15 per instruction at W = 3:
+    the adds do not hide in the mads' extra cycles).
+So for a launch with N_valu VALU, N_int64 64-bit (SQ_INSTS_VALU_INT64: mads included) and N_mad
+multiply-add wave-instructions (N_mad exact from the SOP programs, below):
+    issue fraction   = (C_MAD N_mad + C_64 (N_int64 - N_mad) + C_32 (N_valu - N_int64)) / S
+    (without an INT64 count: C_MAD N_mad + C_32 (N_valu - N_mad), a lower bound)
 with S = GRBM_GUI_ACTIVE / 8 * 1024 the launch's SIMD cycles (GRBM summed over 8 XCDs; DVFS-true).
 
 N_mad per wave-round with K products: K * (147 + 12 mflag) + 196 [K > 0] + 12 nadd — a Karatsuba product
@@ -23,8 +23,7 @@ c * v 12 (csrc/lcv_sop.hpp, lcv_col28.hpp; `--isa` counts them in the compiled k
 
 SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES ("valu_busy", 0.46-0.49 for these kernels) equals SQ_INSTS_VALU /
 SQ_WAVE_CYCLES here (one quad-cycle per instruction): the share of a resident wave's quad-cycles in which
-IT issued a VALU instruction.  With ~1.6 waves per SIMD each wave issues about every second quad-cycle, so
-the SIMD issues ~0.8 per quad-cycle: an issue count per wave, not the pipe's occupancy.
+IT issued a VALU instruction — an issue count per wave, not the pipe's occupancy.
 """
 from __future__ import annotations
 
@@ -35,9 +34,26 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-C_VALU = 4.0   # SIMD cycles per wave64 32-bit VALU instruction (valubench: 4.08-4.3)
-C_MAD = 6.0    # SIMD cycles per wave64 v_mad_u64_u32 issued back to back (valubench: 5.7-6.0)
+PEAK_FILE = os.path.join(ROOT, "profiles", "r05_cal", "peakbench.txt")
 SIMDS = 1024   # 256 CUs x 4 SIMDs
+
+
+def _costs(path: str = PEAK_FILE, w: int = 3) -> tuple:
+    """(C_MAD, C_64, C_32): SIMD cycles per wave64 instruction from the committed peakbench output."""
+    rows = {}
+    for line in open(path):
+        if line.startswith("#") or "|" not in line:
+            continue
+        head, *cols = [c.strip() for c in line.split("|")]
+        name, ww = head.rsplit(None, 1)
+        rows[(name.split()[0], int(ww))] = float(cols[3])  # cycles per instruction at 2.4 GHz (wall)
+    c64 = sum(rows[(k, w)] for k in ("add64", "mullo", "fma64")) / 3
+    adds = sorted(rows[("add", ww)] for ww in (2, 3, 4, 8))
+    return rows[("mad", w)], c64, (adds[1] + adds[2]) / 2
+
+
+C_MAD, C_64, C_32 = _costs()
+C_VALU = C_32  # (name kept for callers: the full-rate class)
 
 # per-construct mad counts of the interpreter (checked against the ISA by --isa)
 MADS_PER_PRODUCT = 147      # one subtractive Karatsuba level: P0, P2 (49 unsigned each) + D (49 signed)
@@ -50,7 +66,18 @@ SOP_KERNELS = {"k_sop<F_sop_lines>": "lines", "k_sop<F_sop_acc>": "miller_acc", 
                "k_sop<F_sop_h2c>": "h2c"}
 
 
+_COUNTS = None
+
+
 def sop_wave_counts() -> dict:
+    """(cached: building the programs takes seconds)"""
+    global _COUNTS
+    if _COUNTS is None:
+        _COUNTS = _sop_wave_counts()
+    return _COUNTS
+
+
+def _sop_wave_counts() -> dict:
     """program name -> {"mads_per_wave", "rounds", "team", "items_per_wave"} from the generator's tables."""
     import gen_sop as G
     out = {}
@@ -81,16 +108,22 @@ def pipe(kernel: str, raw: dict, counts: dict | None = None, c_mad: float = C_MA
         mad_source = "SQ_INSTS_VALU_INT64 (includes the 64-bit shifts / adds: an upper bound)"
     else:
         return None
-    lo = n_valu * c_valu
-    hi = lo + n_mad * (c_mad - c_valu)
+    n64 = raw.get("SQ_INSTS_VALU_INT64")
+    if n64 is not None and n64 >= n_mad:
+        need = c_mad * n_mad + C_64 * (n64 - n_mad) + c_valu * (n_valu - n64)
+        model = "mads x C_MAD + other INT64 x C_64 + the rest x C_32 (peakbench costs)"
+    else:
+        need = c_mad * n_mad + c_valu * (n_valu - n_mad)
+        model = "mads x C_MAD + the rest x C_32 (no INT64 count: a lower bound)"
     avail = raw["GRBM_GUI_ACTIVE"] / 8 * SIMDS
     out = {"valu_insts_per_launch": round(n_valu), "mad_insts_per_launch": round(n_mad),
            "mad_fraction_of_valu_insts": round(n_mad / n_valu, 4),
+           "mad_share_of_pipe_cycles": round(c_mad * n_mad / need, 4),
            "simd_cycles_per_launch": round(avail),
-           "issue_fraction": round(lo / avail, 4), "pipe_utilization_upper": round(hi / avail, 4),
-           "pipe_cycles_per_launch": round(lo), "pipe_cycles_per_launch_upper": round(hi),
-           "c_valu": c_valu, "c_mad_back_to_back": c_mad, "waves_per_launch": round(waves),
-           "mad_count_source": mad_source}
+           "issue_fraction": round(need / avail, 4),
+           "pipe_cycles_per_launch": round(need), "model": model,
+           "c_mad": round(c_mad, 3), "c_64": round(C_64, 3), "c_32": round(c_valu, 3),
+           "waves_per_launch": round(waves), "mad_count_source": mad_source}
     if raw.get("SQ_INSTS_VALU_INT64") is not None:
         out["int64_valu_insts_per_launch"] = round(raw["SQ_INSTS_VALU_INT64"])
     return out
