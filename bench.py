@@ -587,7 +587,7 @@ def latency_lines(v, sb, calls: int = 20) -> dict:
             "fast_aggregate_verify_512_cold_ms": round(1000 * first, 3), "fast_aggregate_verify_valid": bool(fav_ok),
             "note": "batch engine (default); *_latency_engines_ms with lcv_set_latency_mode(32): signature decoding "
                     "and the SSWU maps one update per wave (products spread over the lanes), the SOP programs on "
-                    "the quad engine (four lanes per op) - measured slower, off by default (DESIGN.md 3.5)"}
+                    "the fan engine (an op's K products on K lanes, one update per block; DESIGN.md 3.5)"}
 
 
 def wire_path(v, sb, n: int) -> dict:

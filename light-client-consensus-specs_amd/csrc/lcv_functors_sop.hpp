@@ -10,7 +10,7 @@
 #include "lcv_sop.hpp"
 #include "lcv_sop_programs.inc"
 #if defined(LCV_KERNEL_UNIT)
-#include "lcv_sop_quad.hpp"
+#include "lcv_sop_fan.hpp"
 #endif
 
 enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
@@ -28,6 +28,7 @@ struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t MAXK = LCV_SOP_LINES_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
@@ -99,6 +100,7 @@ struct F_sop_lines {
 struct F_sop_acc {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t MAXK = LCV_SOP_MILLER_ACC_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -125,6 +127,7 @@ struct F_sop_acc {
 struct F_sop_fexp {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t MAXK = LCV_SOP_FEXP_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -169,6 +172,7 @@ struct F_sop_fexp {
 struct F_sop_h2c {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t MAXK = LCV_SOP_H2C_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
@@ -251,40 +255,71 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
   if (active) f.epilogue(item, lane, my);
 }
 
-// The quad engine's round loop (lcv_sop_quad.hpp; latency mode): ONE item per one-wave block, op o of a
-// round on lanes 4o .. 4o + 3 (TEAM <= 16).  LDS: the constants, the item's slots, then per op the
-// 4 x 29 64-bit column scratch of the products' transpose (zeroed once: each lane rewrites the same
-// positions every round, the rest stays zero).
+// The fan engine's round loop (lcv_sop_fan.hpp; latency mode): ONE item per block of TEAM x MAXK lanes
+// (lcv_hip_launch_sop_fan sizes it to whole waves), lane o * MAXK + k computes product k of op o.  LDS:
+// the constants, the q p table, the item's slots, then the ops' column scratch (TEAM x MAXK rows of 28
+// 64-bit columns).  Three block barriers per round: after the products, after the column sums, and
+// between the tails' reads (add-in terms) and their stores (the ops of a round sit in several waves).
 template <class F>
-__global__ __launch_bounds__(64) void k_sop_quad(F f, uint32_t n) {
-  constexpr uint32_t T = F::TEAM;
-  static_assert(T <= 16, "four lanes per op in one wave");
+__global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM, KM = F::MAXK, NT = ((T * KM + 63) / 64) * 64;
   constexpr uint32_t ITEM_WORDS = (F::LDS_WORDS + 1u) & ~1u;  // 8-byte aligned scratch after the slots
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t op = threadIdx.x >> 2, q = threadIdx.x & 3u;
+  const uint32_t L = threadIdx.x, o = L / KM, k = L % KM;
   const uint32_t item = blockIdx.x;
-  const bool active = op < T && item < n;
-  uint32_t* my = lds + F::SHARED_WORDS;
-  uint64_t* scratch = (uint64_t*)(lds + F::SHARED_WORDS + ITEM_WORDS);
-  uint64_t* S = scratch + (op < T ? op : 0) * lcv::QUAD_SCRATCH_U64;
-  for (uint32_t k = threadIdx.x; k < F::SHARED_WORDS; k += 64) lds[k] = f.P.consts[k];
-  for (uint32_t k = threadIdx.x; k < T * lcv::QUAD_SCRATCH_U64; k += 64) scratch[k] = 0;
-  if (active && q == 0) f.prologue(item, op, my);
+  const bool active = o < T && item < n;
+  uint32_t* qp = lds + F::SHARED_WORDS;
+  uint32_t* my = qp + lcv::SOP_QP_WORDS;
+  uint64_t* S = (uint64_t*)(my + ITEM_WORDS);
+  uint64_t* row = S + (size_t)(active ? o * KM : 0) * lcv::FAN_COLS;  // row j of op o: row + 28 j
+  for (uint32_t x = L; x < F::SHARED_WORDS; x += NT) lds[x] = f.P.consts[x];
+  if (L < lcv::SOP_QP_N) lcv::sop_qp_entry(qp + 16 * L, L);
+  if (L < T && item < n) f.prologue(item, L, my);
   __syncthreads();
-  uint32_t pz[16];
-  lcv::quad_ptable(pz, q);
-  const uint32_t* io_in = active ? f.io_in(item) : nullptr;
-  uint32_t* io_out = active ? f.io_out(item) : nullptr;
+  const uint32_t* io_in = item < n ? f.io_in(item) : nullptr;
+  uint32_t* io_out = item < n ? f.io_out(item) : nullptr;
   const uint32_t R = f.P.rounds, ns = f.P.nslots;
+  const lcv::SopBase base{my, lds, (int32_t)((const char*)lds - (const char*)my)};
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
     const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 1]);
     const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
     const uint32_t h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 3]);
-    const uint32_t* w = f.P.rec + off + (active ? op : 0) * words;
-    if (active) lcv::sop_exec_quad(h0, h3, w, lcv::sop_pre(h0, w), my, my, lds, ns, io_in, io_out, q, S, pz);
+    const uint32_t K = h0 & 15u;
+    const uint32_t* w = f.P.rec + off + (active ? o : 0) * words;
+    if (active && k < K) {
+      uint64_t col[28];
+      lcv::sop_fan_product(col, w, k, h3, (h0 >> 6) & 1u, base);
+      uint64_t* dst = row + (size_t)k * lcv::FAN_COLS;
+      LCV_UNROLL for (int c = 0; c < 28; ++c) dst[c] = col[c];
+    }
+    __syncthreads();
+    if (active && k < K && K > 1) {  // columns c = k, k + K, ... summed over the op's K rows into row 0
+      for (uint32_t c = k; c < lcv::FAN_COLS; c += K) {
+        uint64_t s = row[c];
+        for (uint32_t j = 1; j < K; ++j) s += row[(size_t)j * lcv::FAN_COLS + c];
+        row[c] = s;
+      }
+    }
+    __syncthreads();
+    lcv::fp v;
+    lcv::SopPre pre{0, 0, 0, 0, 0};
+    if (active && k == 0) {
+      pre = lcv::sop_pre(h0, w);
+      uint32_t res[13];
+      if (K == 0) {
+        LCV_UNROLL for (int j = 0; j < 13; ++j) res[j] = 0;
+      } else {
+        uint64_t col[28];
+        LCV_UNROLL for (int c = 0; c < 28; ++c) col[c] = row[c];
+        lcv::sop_redc28(res, col);
+      }
+      lcv::sop_tail_value(v, h0, w, pre, my, lds, ns, res, qp);
+    }
+    __syncthreads();
+    if (active && k == 0) lcv::sop_tail_store(h0, pre, my, io_in, io_out, v);
     __syncthreads();
   }
-  if (active && q == 0) f.epilogue(item, op, my);
+  if (L < T && item < n) f.epilogue(item, L, my);
 }
 #endif

@@ -56,7 +56,7 @@ static int be_nstreams() { return BE_STREAMS; }
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
-template <class F> static int be_launch_sop_quad(lcv_ctx* ctx, const F& f, uint32_t n);
+template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n);
 static int be_fork(lcv_ctx* ctx);
 static int be_join(lcv_ctx* ctx);
@@ -247,10 +247,10 @@ template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n
   return LCV_OK;
 }
 
-template <class F> static int be_launch_sop_quad(lcv_ctx* ctx, const F& f, uint32_t n) {
+template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n) {
   if (n == 0) return LCV_OK;
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  HIPCHK(ctx, lcv_hip_launch_sop_quad<F>(f, n, cur_stream(ctx)));  // lcv_k_quad.hip
+  HIPCHK(ctx, lcv_hip_launch_sop_fan<F>(f, n, cur_stream(ctx)));  // lcv_k_fan.hip
   return LCV_OK;
 }
 template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n) {

@@ -52,8 +52,8 @@ template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t 
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
 // the latency engine's launches run the same per-item code (the device spreads products over lanes)
 template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch(ctx, f, n); }
-// the quad engine (device latency mode) computes the batch engine's values: the simulation runs the latter
-template <class F> static int be_launch_sop_quad(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch_sop(ctx, f, n); }
+// the fan engine (device latency mode) computes the batch engine's values: the simulation runs the latter
+template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch_sop(ctx, f, n); }
 static int be_fork(lcv_ctx*) { return 0; }
 static int be_join(lcv_ctx*) { return 0; }
 static void be_use_stream(lcv_ctx* ctx, int k);

@@ -10,7 +10,7 @@
 template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t s);
 template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s);
 template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s, uint32_t g = 0);
-template <class F> hipError_t lcv_hip_launch_sop_quad(const F& f, uint32_t n, hipStream_t s);
+template <class F> hipError_t lcv_hip_launch_sop_fan(const F& f, uint32_t n, hipStream_t s);
 // the latency engine (lcv_k_wide.hip): one item per wave, products spread over the lanes
 template <class F> hipError_t lcv_hip_launch_wide(const F& f, uint32_t n, hipStream_t s);
 
@@ -61,16 +61,17 @@ template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStre
   hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), lds_bytes, s, f, n, g);
   return hipGetLastError();
 }
-// the quad engine (latency mode, lcv_sop_quad.hpp): one item per one-wave block, 4 lanes per op
-template <class F> __global__ void k_sop_quad(F f, uint32_t n);
-template <class F> hipError_t lcv_hip_launch_sop_quad(const F& f, uint32_t n, hipStream_t s) {
-  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + ((F::LDS_WORDS + 1u) & ~1u)) +
-                           8 * (size_t)F::TEAM * 4 * 29;
-  hipLaunchKernelGGL(k_sop_quad<F>, dim3(n), dim3(64), lds_bytes, s, f, n);
+// the fan engine (latency mode, lcv_sop_fan.hpp): one item per block of TEAM x MAXK lanes (whole waves)
+template <class F> __global__ void k_sop_fan(F f, uint32_t n);
+template <class F> hipError_t lcv_hip_launch_sop_fan(const F& f, uint32_t n, hipStream_t s) {
+  constexpr uint32_t NT = ((F::TEAM * F::MAXK + 63) / 64) * 64;
+  const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + LCV_SOP_QP_WORDS + ((F::LDS_WORDS + 1u) & ~1u)) +
+                           8 * (size_t)F::TEAM * F::MAXK * 28;
+  hipLaunchKernelGGL(k_sop_fan<F>, dim3(n), dim3(NT), lds_bytes, s, f, n);
   return hipGetLastError();
 }
 #define LCV_INSTANTIATE_SOP(F) template hipError_t lcv_hip_launch_sop<F>(const F&, uint32_t, hipStream_t, uint32_t);
-#define LCV_INSTANTIATE_SOP_QUAD(F) template hipError_t lcv_hip_launch_sop_quad<F>(const F&, uint32_t, hipStream_t);
+#define LCV_INSTANTIATE_SOP_FAN(F) template hipError_t lcv_hip_launch_sop_fan<F>(const F&, uint32_t, hipStream_t);
 #define LCV_INSTANTIATE(F) template hipError_t lcv_hip_launch<F>(const F&, uint32_t, hipStream_t);
 #define LCV_INSTANTIATE_TEAM(F) template hipError_t lcv_hip_launch_team<F>(const F&, uint32_t, hipStream_t);
 #endif

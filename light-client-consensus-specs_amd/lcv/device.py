@@ -146,9 +146,11 @@ class Verifier:
         self._check(self.lib.lcv_set_pipeline(self.ctx, int(streams), int(chunks)), "lcv_set_pipeline")
 
     def set_latency_mode(self, max_rows: int) -> None:
-        """Batches of at most max_rows rows decode signatures and run the SSWU maps on the latency engine
-        (one item per wave, products spread over the lanes; identical results); 0 = the batch engine
-        always (default 32)."""
+        """Latency engines for small batches (lcv_set_latency_mode): batches of at most max_rows rows decode
+        signatures and run the SSWU maps one item per wave (products spread over the lanes), and run the SOP
+        programs (Miller lines and accumulation, final exponentiation, hash_to_G2's tail) on the fan engine
+        (an op's K products on K lanes, one item per block).  Results are identical to the batch engine's.
+        0 (the default) = the batch engine always."""
         self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
         self.latency_mode = int(max_rows)
 

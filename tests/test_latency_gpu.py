@@ -1,10 +1,10 @@
 """The latency engines (opt-in: lcv_set_latency_mode(max_rows > 0); off by default): batches of at most
 max_rows rows run signature decoding and the SSWU maps one item per wave with every Montgomery product
 spread over the wave's lanes (csrc/lcv_k_wide.hip, fp_mul_wide), and the SOP programs — Miller lines and
-accumulation, final exponentiation, hash_to_G2's tail — on the quad engine, four lanes per op and one
-item per wave (csrc/lcv_k_quad.hip, lcv_sop_quad.hpp).  Their results must equal the batch engine's bit
-for bit and the oracle's: verdicts and reasons on adversarial rows, decoded signatures, hash_to_G2 points
-and pairing values."""
+accumulation, final exponentiation, hash_to_G2's tail — on the fan engine, an op's K products on K lanes
+and one item per block (csrc/lcv_k_fan.hip, lcv_sop_fan.hpp).  Their results must equal the batch engine's
+bit for bit and the oracle's: verdicts and reasons on adversarial rows, decoded signatures, hash_to_G2
+points and pairing values."""
 import random
 
 import numpy as np

@@ -45,12 +45,19 @@ def _v(w, n=12):
     return sum(int(w[i]) << (32 * i) for i in range(n))
 
 
-@pytest.mark.parametrize("red", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("red", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_sop_reduce_exact(lib, red):
+    """Every multiple k p (and its neighbourhood) for red <= 5; for red 6..10 (tools/gen_sop.py allows
+    red <= 10, the error analysis needs q < 2^15) sampled multiples: the smallest and the largest 24, and
+    100 random k."""
     rng = random.Random(100 + red)
     top = (1 << red) * P
     vals = [0, 1, P - 1, top - 1, top - P]
-    for k in range(1, 1 << red):
+    ks = range(1, 1 << red)
+    if red > 5:
+        ks = sorted(set(list(range(1, 25)) + list(range((1 << red) - 24, 1 << red)) +
+                        [rng.randrange(1, 1 << red) for _ in range(100)]))
+    for k in ks:
         vals += [k * P - 1, k * P, k * P + 1, k * P + (1 << 320) - 1, k * P - (1 << 320),
                  k * P + rng.randrange(1 << 64), k * P - rng.randrange(1, 1 << 64)]
         # around the device's skip threshold (fractional part of the estimate within ~2^-29 of 1)
