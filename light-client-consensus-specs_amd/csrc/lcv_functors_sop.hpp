@@ -256,24 +256,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
 }
 
 // The fan engine's round loop (lcv_sop_fan.hpp; latency mode): ONE item per block of TEAM x MAXK lanes
-// (lcv_hip_launch_sop_fan sizes it to whole waves), lane o * MAXK + k computes product k of op o.  LDS:
-// the constants, the q p table, the item's slots, then the ops' column scratch (TEAM x MAXK rows of 28
-// 64-bit columns).  Three block barriers per round: after the products, after the column sums, and
-// between the tails' reads (add-in terms) and their stores (the ops of a round sit in several waves).
+// (lcv_hip_launch_sop_fan sizes it to whole waves), lane k * TEAM + o computes product k of op o, so the
+// ops' product-0 lanes — which also run the reductions and tails — are lanes 0 .. TEAM - 1 of the first
+// wave, whose lockstep orders every tail's reads before any store.  The products' joined columns meet in
+// the op's 28-column LDS accumulator by 64-bit LDS atomic adds (ds_add_u64); the op's tail lane reads the
+// sums and zeroes the accumulator for the next round.  Two block barriers per round: after the products
+// (the sums are complete) and after the stores (the next round reads them).
 template <class F>
 __global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
   constexpr uint32_t T = F::TEAM, KM = F::MAXK, NT = ((T * KM + 63) / 64) * 64;
   constexpr uint32_t ITEM_WORDS = (F::LDS_WORDS + 1u) & ~1u;  // 8-byte aligned scratch after the slots
+  static_assert(T <= 64, "every op's tail lane in the first wave");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t L = threadIdx.x, o = L / KM, k = L % KM;
+  const uint32_t L = threadIdx.x, k = L / T, o = L % T;
   const uint32_t item = blockIdx.x;
-  const bool active = o < T && item < n;
+  const bool active = k < KM && item < n;
   uint32_t* qp = lds + F::SHARED_WORDS;
   uint32_t* my = qp + lcv::SOP_QP_WORDS;
-  uint64_t* S = (uint64_t*)(my + ITEM_WORDS);
-  uint64_t* row = S + (size_t)(active ? o * KM : 0) * lcv::FAN_COLS;  // row j of op o: row + 28 j
+  uint64_t* acc = (uint64_t*)(my + ITEM_WORDS) + (size_t)o * lcv::FAN_COLS;  // op o's column accumulator
   for (uint32_t x = L; x < F::SHARED_WORDS; x += NT) lds[x] = f.P.consts[x];
   if (L < lcv::SOP_QP_N) lcv::sop_qp_entry(qp + 16 * L, L);
+  if (L < T) LCV_UNROLL for (int c = 0; c < 28; ++c) acc[c] = 0;
   if (L < T && item < n) f.prologue(item, L, my);
   __syncthreads();
   const uint32_t* io_in = item < n ? f.io_in(item) : nullptr;
@@ -286,38 +289,28 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fa
     const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
     const uint32_t h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 3]);
     const uint32_t K = h0 & 15u;
-    const uint32_t* w = f.P.rec + off + (active ? o : 0) * words;
+    const uint32_t* w = f.P.rec + off + o * words;
     if (active && k < K) {
       uint64_t col[28];
       lcv::sop_fan_product(col, w, k, h3, (h0 >> 6) & 1u, base);
-      uint64_t* dst = row + (size_t)k * lcv::FAN_COLS;
-      LCV_UNROLL for (int c = 0; c < 28; ++c) dst[c] = col[c];
+      LCV_UNROLL for (int c = 0; c < 28; ++c) __hip_atomic_fetch_add(acc + c, col[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
-    if (active && k < K && K > 1) {  // columns c = k, k + K, ... summed over the op's K rows into row 0
-      for (uint32_t c = k; c < lcv::FAN_COLS; c += K) {
-        uint64_t s = row[c];
-        for (uint32_t j = 1; j < K; ++j) s += row[(size_t)j * lcv::FAN_COLS + c];
-        row[c] = s;
-      }
-    }
-    __syncthreads();
-    lcv::fp v;
-    lcv::SopPre pre{0, 0, 0, 0, 0};
-    if (active && k == 0) {
-      pre = lcv::sop_pre(h0, w);
+    if (L < T && item < n) {  // op o's tail, in the first wave: every read of the round precedes its stores
+      const lcv::SopPre pre = lcv::sop_pre(h0, w);
       uint32_t res[13];
       if (K == 0) {
         LCV_UNROLL for (int j = 0; j < 13; ++j) res[j] = 0;
       } else {
         uint64_t col[28];
-        LCV_UNROLL for (int c = 0; c < 28; ++c) col[c] = row[c];
+        LCV_UNROLL for (int c = 0; c < 28; ++c) col[c] = acc[c];
+        LCV_UNROLL for (int c = 0; c < 28; ++c) acc[c] = 0;
         lcv::sop_redc28(res, col);
       }
+      lcv::fp v;
       lcv::sop_tail_value(v, h0, w, pre, my, lds, ns, res, qp);
+      lcv::sop_tail_store(h0, pre, my, io_in, io_out, v);
     }
-    __syncthreads();
-    if (active && k == 0) lcv::sop_tail_store(h0, pre, my, io_in, io_out, v);
     __syncthreads();
   }
   if (L < T && item < n) f.epilogue(item, L, my);

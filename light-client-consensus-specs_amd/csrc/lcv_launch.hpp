@@ -66,7 +66,7 @@ template <class F> __global__ void k_sop_fan(F f, uint32_t n);
 template <class F> hipError_t lcv_hip_launch_sop_fan(const F& f, uint32_t n, hipStream_t s) {
   constexpr uint32_t NT = ((F::TEAM * F::MAXK + 63) / 64) * 64;
   const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + LCV_SOP_QP_WORDS + ((F::LDS_WORDS + 1u) & ~1u)) +
-                           8 * (size_t)F::TEAM * F::MAXK * 28;
+                           8 * (size_t)F::TEAM * 28;
   hipLaunchKernelGGL(k_sop_fan<F>, dim3(n), dim3(NT), lds_bytes, s, f, n);
   return hipGetLastError();
 }

@@ -1,17 +1,16 @@
 // lcv_sop_fan.hpp — the fan engine: the SOP programs (lcv_sop.hpp, tools/gen_sop.py) with the K products
 // of every op fanned out over K lanes, for the latency path (lcv_set_latency_mode: batches of a few
 // updates, the reference's one-update-per-call usage, sync-protocol.md:512 -> :464).  One item per block
-// of TEAM x MAXK lanes (up to three waves); lane o * MAXK + k computes product k of op o.
+// of TEAM x MAXK lanes (up to three waves); lane k * TEAM + o computes product k of op o.
 //
 // A lone item pays the latency of every instruction of a round: on the batch engine one lane runs an op's
 // K products back to back (K x ~150 multiply-adds plus operand conversion) and then its reduction, so an
 // op of K = 7 (the Miller accumulation's Fp12 squaring) costs ~7 products of latency.  Here a round is
 //   products   lane (o, k) forms X_k, Y_k and their Karatsuba columns (lcv_col28.hpp), joined: 28 true
-//              column sums of X_k Y_k, written to the op's LDS scratch row k;
-//   sum        lane (o, k) adds rows 0..K-1 of the columns c = k, k + K, ... into row 0 (block barrier
-//              before and after);
-//   reduce     lane (o, 0) reads the 28 summed columns, runs the batch engine's Montgomery reduction and
-//              its tail (add-ins, conditional subtractions, store, shadow: lcv::sop_tail).
+//              column sums of X_k Y_k, added into the op's 28-column LDS accumulator (64-bit LDS atomics);
+//   reduce     after a block barrier, lane (o, 0) — the first wave holds every op's — reads the sums,
+//              zeroes the accumulator, runs the batch engine's Montgomery reduction and its tail (add-ins,
+//              conditional subtractions, store, shadow: lcv::sop_tail).
 // The column sums are the batch engine's exactly (the join is linear and every joined column is a true,
 // non-negative column sum below the op's bound), so every result is the batch engine's bit for bit
 // (tests/test_latency_gpu.py).  Device-only; the host simulation runs the batch engine.
@@ -20,7 +19,7 @@
 
 namespace lcv {
 
-enum : uint32_t { FAN_COLS = 28 };
+enum : uint32_t { FAN_COLS = 28 };  // 64-bit columns of an op's LDS accumulator
 
 // product k of the op whose record is w (K > 0, k < K): its 28 joined columns
 LCV_FN void sop_fan_product(uint64_t col[28], const uint32_t* w, uint32_t k, uint32_t masks, bool mflag,
