@@ -569,9 +569,9 @@ def latency_lines(v, sb, calls: int = 20) -> dict:
         t0 = time.perf_counter()
         fav_ok &= v.fast_aggregate_verify(pks, msg, sig)
         tf.append(time.perf_counter() - t0)
-    # the same single-update call on the opt-in latency engines (lcv_set_latency_mode(32))
-    prev = getattr(v, "latency_mode", 0)
-    v.set_latency_mode(32)
+    # the same single-update call on the batch engine (lcv_set_latency_mode(0)), for comparison
+    prev = getattr(v, "latency_mode", 64)
+    v.set_latency_mode(0)
     try:
         v.validate(one, sb.current_slot, gvr)
         tb = []
@@ -582,12 +582,12 @@ def latency_lines(v, sb, calls: int = 20) -> dict:
     finally:
         v.set_latency_mode(prev)
     return {"validate_one_update_ms": round(1000 * float(np.median(ts)), 3), "validate_one_update_valid": bool(ok[0]),
-            "validate_one_update_latency_engines_ms": round(1000 * float(np.median(tb)), 3),
+            "validate_one_update_batch_engine_ms": round(1000 * float(np.median(tb)), 3),
             "fast_aggregate_verify_512_ms": round(1000 * float(np.median(tf)), 3),
             "fast_aggregate_verify_512_cold_ms": round(1000 * first, 3), "fast_aggregate_verify_valid": bool(fav_ok),
-            "note": "batch engine (default); *_latency_engines_ms with lcv_set_latency_mode(32): signature decoding "
-                    "and the SSWU maps one update per wave (products spread over the lanes), the SOP programs on "
-                    "the fan engine (an op's K products on K lanes, one update per block; DESIGN.md 3.5)"}
+            "note": "default latency mode (lcv_set_latency_mode 64: the SOP programs of batches <= 64 rows on the "
+                    "fan engine, an op's K products on K lanes, one update per block; DESIGN.md 3.5); "
+                    "*_batch_engine_ms: the same call with latency mode off"}
 
 
 def wire_path(v, sb, n: int) -> dict:

@@ -4,6 +4,8 @@
 #pragma once
 // work-space slots of a context (up to eight batches in flight) and the events that order a slot's two streams
 enum { LCV_SLOTS = 8 };
+// lcv_set_latency_mode's default: batches of at most this many rows run the SOP programs on the fan engine
+enum : unsigned long long { LCV_FAN_MAX_DEFAULT = 64 };
 enum { EV_START = 0, EV_PRE, EV_H2C, EV_SIDE, EV_H2D, EV_COUNT };  // EV_H2D: the slot's staged batch has left host memory
 #include <stddef.h>
 #include <stdint.h>

@@ -213,95 +213,6 @@ LCV_FN void fp_sqr_c28r(uint32_t r[12], const uint32_t a[12]) {
 #define LCV_MUL_IMPL fp_mul_ps
 #endif
 
-// ---- The wide engine (latency mode): ONE item per wave, its values replicated in every lane, and each
-// Montgomery product spread over the lanes — lane c accumulates column c of the 24-column product (12
-// multiply-accumulates instead of 144), the column sums are normalised into words by wave-wide DPP
-// shifts (wave_shr:1) with a ballot-terminated carry ripple, and the reduction is the separated form
-// M = (T mod R) N' mod R, U = T + M p (each again column-per-lane), r = U / R.  M is the unique M < R
-// with T + M p = 0 mod R, so r equals the interleaved (CIOS / product-scanning) result bit for bit.
-// Lanes read the staged operand and the constant tables from per-wave LDS (wide_lds): words [16, 28)
-// hold the value, every other word of the 80-word window is zero, so lane c reads word 16 + c - i.
-enum { WIDE_WIN = 80, WIDE_MAX_WAVES = 16, WIDE_OFF = 16 };
-__shared__ uint32_t wide_lds[2 * WIDE_WIN + WIDE_MAX_WAVES * WIDE_WIN];  // [N' table][p table][per-wave operand]
-
-LCV_FN uint32_t wide_lane() { return __lane_id(); }
-LCV_FN uint32_t* wide_scratch() { return wide_lds + 2 * WIDE_WIN + (threadIdx.x >> 6) * WIDE_WIN; }
-LCV_FN uint32_t wide_shr1(uint32_t x) { return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xf, 0xf, false); }
-
-// every wide kernel starts with this (before its first wide product): constant tables + zeroed windows
-LCV_FN void wide_init() {
-  constexpr uint32_t PL[12] = LCV_P_INIT;
-  constexpr uint32_t NP[12] = LCV_NPFULL_INIT;
-  for (uint32_t k = threadIdx.x; k < 2 * WIDE_WIN + WIDE_MAX_WAVES * WIDE_WIN; k += blockDim.x) {
-    uint32_t v = 0;
-    LCV_UNROLL for (int j = 0; j < 12; ++j) {
-      if (k == (uint32_t)(WIDE_OFF + j)) v = NP[j];
-      if (k == (uint32_t)(WIDE_WIN + WIDE_OFF + j)) v = PL[j];
-    }
-    wide_lds[k] = v;
-  }
-  __syncthreads();
-}
-
-// column sums (hi:acc, 96 bits, lanes 0..L-1; lanes >= L ignored) -> this lane's 32-bit word of the sum
-// (words >= L of the sum are dropped: callers size L so the value fits, or want it mod 2^(32 L))
-template <uint32_t L>
-LCV_FN uint32_t wide_norm(uint64_t acc, uint32_t hi) {
-  const uint32_t lane = wide_lane();
-  const uint32_t w1 = wide_shr1((uint32_t)(acc >> 32));
-  const uint32_t w2 = wide_shr1(wide_shr1(hi));
-  uint32_t c1, c2;
-  uint32_t t = addc32((uint32_t)acc, w1, 0u, c1);
-  t = addc32(t, w2, 0u, c2);
-  uint32_t cy = lane < L ? c1 + c2 : 0u;
-  while (__builtin_amdgcn_ballot_w64(cy != 0u)) {
-    const uint32_t cin = wide_shr1(cy);
-    t = addc32(t, cin, 0u, cy);
-    cy = lane < L ? cy : 0u;
-  }
-  return t;
-}
-
-// distributed T (lane c: word c, c < 25) -> r = (T + M p) / R (13 words, replicated), M = (T mod R) N' mod R
-LCV_FN void wide_redc(uint32_t r[13], uint32_t T) {
-  const uint32_t lane = wide_lane();
-  const uint32_t* np = wide_lds + WIDE_OFF + lane;
-  const uint32_t* pp = wide_lds + WIDE_WIN + WIDE_OFF + lane;
-  uint64_t acc = 0;
-  uint32_t hi = 0;
-  LCV_UNROLL for (int i = 0; i < 12; ++i) mac_vs(acc, hi, np[-i], __builtin_amdgcn_readlane(T, i));
-  const uint32_t M = wide_norm<12>(acc, hi);
-  acc = T;
-  hi = 0;
-  LCV_UNROLL for (int i = 0; i < 12; ++i) mac_vs(acc, hi, pp[-i], __builtin_amdgcn_readlane(M, i));
-  const uint32_t U = wide_norm<25>(acc, hi);
-  LCV_UNROLL for (int j = 0; j < 13; ++j) r[j] = __builtin_amdgcn_readlane(U, 12 + j);
-}
-
-// r = a b R^-1 mod p, a, b < 2p replicated in every lane of the wave (the result replicated, fully
-// reduced: identical to fp_mul_ps)
-LCV_FN void fp_mul_wide(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
-  const uint32_t lane = wide_lane();
-  uint32_t* bs = wide_scratch();
-  __builtin_amdgcn_wave_barrier();  // (a wave's LDS accesses run in program order: compiler ordering only)
-  if (lane == 0) {
-    LCV_UNROLL for (int j = 0; j < 12; ++j) bs[WIDE_OFF + j] = b[j];
-  }
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t* bl = bs + WIDE_OFF + lane;
-  uint64_t acc = 0;
-  uint32_t hi = 0;
-  LCV_UNROLL for (int i = 0; i < 12; ++i) mac_vv(acc, hi, a[i], bl[-i]);
-  const uint32_t T = wide_norm<24>(acc, hi);
-  uint32_t u[13];
-  wide_redc(u, T);
-  fp_reduce_once(r, u);
-}
-#if defined(LCV_WIDE)
-#undef LCV_SQR_IMPL
-#undef LCV_MUL_IMPL
-#define LCV_MUL_IMPL fp_mul_wide
-#endif
 #elif defined(LCV_CPU_FAST)
 // CPU-baseline build only (liblcv_cpu.so, bench.py's cpu_baseline leg): the same Montgomery product
 // (R = 2^384, identical representation and results) on 6 x 64-bit limbs with 128-bit products, the

@@ -57,7 +57,6 @@ template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n);
-template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n);
 static int be_fork(lcv_ctx* ctx);
 static int be_join(lcv_ctx* ctx);
 static void be_use_stream(lcv_ctx* ctx, int k);
@@ -251,12 +250,6 @@ template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32
   if (n == 0) return LCV_OK;
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
   HIPCHK(ctx, lcv_hip_launch_sop_fan<F>(f, n, cur_stream(ctx)));  // lcv_k_fan.hip
-  return LCV_OK;
-}
-template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n) {
-  if (n == 0) return LCV_OK;
-  HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  HIPCHK(ctx, lcv_hip_launch_wide<F>(f, n, cur_stream(ctx)));  // lcv_k_wide.hip
   return LCV_OK;
 }
 

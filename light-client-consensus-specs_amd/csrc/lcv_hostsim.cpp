@@ -51,7 +51,6 @@ template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
 // the latency engine's launches run the same per-item code (the device spreads products over lanes)
-template <class F> static int be_launch_wide(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch(ctx, f, n); }
 // the fan engine (device latency mode) computes the batch engine's values: the simulation runs the latter
 template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch_sop(ctx, f, n); }
 static int be_fork(lcv_ctx*) { return 0; }

@@ -11,8 +11,6 @@ template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t
 template <class F> hipError_t lcv_hip_launch_team(const F& f, uint32_t n, hipStream_t s);
 template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStream_t s, uint32_t g = 0);
 template <class F> hipError_t lcv_hip_launch_sop_fan(const F& f, uint32_t n, hipStream_t s);
-// the latency engine (lcv_k_wide.hip): one item per wave, products spread over the lanes
-template <class F> hipError_t lcv_hip_launch_wide(const F& f, uint32_t n, hipStream_t s);
 
 #ifdef LCV_KERNEL_UNIT
 template <class F>

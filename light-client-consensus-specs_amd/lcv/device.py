@@ -112,7 +112,7 @@ class Verifier:
             raise LcvError(f"lcv_init(device={device}) failed with status {rc}")
         self.device = device
         self.config = _config.MAINNET  # the context's network configuration (lcv_init: mainnet)
-        self.latency_mode = 0  # lcv_set_latency_mode's value (lcv_init's default: batch engine always)
+        self.latency_mode = 64  # lcv_set_latency_mode's value (lcv_init's default: the fan engine up to 64 rows)
 
     # ------------------------------------------------------------------ plumbing
     def _check(self, rc: int, what: str):
@@ -146,11 +146,10 @@ class Verifier:
         self._check(self.lib.lcv_set_pipeline(self.ctx, int(streams), int(chunks)), "lcv_set_pipeline")
 
     def set_latency_mode(self, max_rows: int) -> None:
-        """Latency engines for small batches (lcv_set_latency_mode): batches of at most max_rows rows decode
-        signatures and run the SSWU maps one item per wave (products spread over the lanes), and run the SOP
+        """Latency mode for small batches (lcv_set_latency_mode): batches of at most max_rows rows run the SOP
         programs (Miller lines and accumulation, final exponentiation, hash_to_G2's tail) on the fan engine
-        (an op's K products on K lanes, one item per block).  Results are identical to the batch engine's.
-        0 (the default) = the batch engine always."""
+        (an op's K products on K lanes, one item per block) — one update 6.4 -> 5.0 ms.  Results are identical
+        to the batch engine's.  Default 64; 0 = the batch engine always."""
         self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
         self.latency_mode = int(max_rows)
 

@@ -1,10 +1,8 @@
-"""The latency engines (opt-in: lcv_set_latency_mode(max_rows > 0); off by default): batches of at most
-max_rows rows run signature decoding and the SSWU maps one item per wave with every Montgomery product
-spread over the wave's lanes (csrc/lcv_k_wide.hip, fp_mul_wide), and the SOP programs — Miller lines and
-accumulation, final exponentiation, hash_to_G2's tail — on the fan engine, an op's K products on K lanes
-and one item per block (csrc/lcv_k_fan.hip, lcv_sop_fan.hpp).  Their results must equal the batch engine's
-bit for bit and the oracle's: verdicts and reasons on adversarial rows, decoded signatures, hash_to_G2
-points and pairing values."""
+"""Latency mode (lcv_set_latency_mode(max_rows); default 64): batches of at most max_rows rows run the SOP
+programs — Miller lines and accumulation, final exponentiation, hash_to_G2's tail — on the fan engine, an
+op's K products on K lanes and one item per block (csrc/lcv_k_fan.hip, lcv_sop_fan.hpp).  Its results must
+equal the batch engine's bit for bit and the oracle's: verdicts and reasons on adversarial rows, decoded
+signatures, hash_to_G2 points and pairing values."""
 import random
 
 import numpy as np
@@ -17,13 +15,16 @@ pytestmark = pytest.mark.gpu
 
 
 def _both(v, fn):
-    """(latency engines on, batch engine) results of fn; leaves the default (0) set."""
-    v.set_latency_mode(32)
+    """(fan engine, batch engine) results of fn; restores the mode it found."""
+    prev = getattr(v, "latency_mode", 64)
+    v.set_latency_mode(64)
     try:
-        wide = fn()
-    finally:
+        fan = fn()
         v.set_latency_mode(0)
-    return wide, fn()
+        batch = fn()
+    finally:
+        v.set_latency_mode(prev)
+    return fan, batch
 
 
 def test_latency_engine_verdicts(gpu_verifier):
@@ -35,14 +36,15 @@ def test_latency_engine_verdicts(gpu_verifier):
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     (okw, rw), (okn, rn) = _both(v, lambda: v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root))
     assert np.array_equal(rw, sb.expected_reason) and np.array_equal(rn, rw) and np.array_equal(okw, okn)
-    # one update at a time (the reference's per-update call, sync-protocol.md:512), on the latency engines
-    v.set_latency_mode(32)
+    # one update at a time (the reference's per-update call, sync-protocol.md:512), on the fan engine
+    prev = getattr(v, "latency_mode", 64)
+    v.set_latency_mode(64)
     try:
         for i in (0, int(np.argmax(sb.expected_reason == 14)) if (sb.expected_reason == 14).any() else 1):
             ok1, r1 = v.validate(sb.updates.slice(i, i + 1), sb.current_slot, sb.genesis_validators_root)
             assert int(r1[0]) == int(sb.expected_reason[i])
     finally:
-        v.set_latency_mode(0)
+        v.set_latency_mode(prev)
 
 
 def test_latency_engine_intermediates(gpu_verifier):
