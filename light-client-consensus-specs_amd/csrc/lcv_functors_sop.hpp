@@ -283,21 +283,38 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fa
   uint32_t* io_out = item < n ? f.io_out(item) : nullptr;
   const uint32_t R = f.P.rounds, ns = f.P.nslots;
   const lcv::SopBase base{my, lds, (int32_t)((const char*)lds - (const char*)my)};
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
+  // round r + 1's header and this lane's record words (its product's operand pair and scale; the tail
+  // lane's dst / io words) are loaded at the top of round r, so their latency overlaps round r's work
+  struct Rec { uint32_t h0, h3, x, y, m; lcv::SopPre pre; const uint32_t* w; };
+  auto fetch = [&](uint32_t r) {
+    Rec c;
+    c.h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
     const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 1]);
     const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
-    const uint32_t h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 3]);
-    const uint32_t K = h0 & 15u;
-    const uint32_t* w = f.P.rec + off + o * words;
+    c.h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 3]);
+    c.w = f.P.rec + off + o * words;
+    const uint32_t K = c.h0 & 15u;
+    c.x = c.y = c.m = 0;
+    if (active && k < K) {
+      const uint32_t* pw = c.w + 4 + 3 * k;
+      c.x = pw[0]; c.y = pw[1]; c.m = pw[2];
+    }
+    c.pre = lcv::SopPre{0, 0, 0, 0, 0};
+    if (L < T && item < n) c.pre = lcv::sop_pre(c.h0, c.w);
+    return c;
+  };
+  Rec nx = fetch(0);
+  for (uint32_t r = 0; r < R; ++r) {
+    const Rec cur = nx;
+    if (r + 1 < R) nx = fetch(r + 1);
+    const uint32_t h0 = cur.h0, K = h0 & 15u;
     if (active && k < K) {
       uint64_t col[28];
-      lcv::sop_fan_product(col, w, k, h3, (h0 >> 6) & 1u, base);
+      lcv::sop_fan_product(col, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, base);
       LCV_UNROLL for (int c = 0; c < 28; ++c) __hip_atomic_fetch_add(acc + c, col[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
     if (L < T && item < n) {  // op o's tail, in the first wave: every read of the round precedes its stores
-      const lcv::SopPre pre = lcv::sop_pre(h0, w);
       uint32_t res[13];
       if (K == 0) {
         LCV_UNROLL for (int j = 0; j < 13; ++j) res[j] = 0;
@@ -308,8 +325,8 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fa
         lcv::sop_redc28(res, col);
       }
       lcv::fp v;
-      lcv::sop_tail_value(v, h0, w, pre, my, lds, ns, res, qp);
-      lcv::sop_tail_store(h0, pre, my, io_in, io_out, v);
+      lcv::sop_tail_value(v, h0, cur.w, cur.pre, my, lds, ns, res, qp);
+      lcv::sop_tail_store(h0, cur.pre, my, io_in, io_out, v);
     }
     __syncthreads();
   }

@@ -21,11 +21,9 @@ namespace lcv {
 
 enum : uint32_t { FAN_COLS = 28 };  // 64-bit columns of an op's LDS accumulator
 
-// product k of the op whose record is w (K > 0, k < K): its 28 joined columns
-LCV_FN void sop_fan_product(uint64_t col[28], const uint32_t* w, uint32_t k, uint32_t masks, bool mflag,
-                            const SopBase& base) {
-  const uint32_t* pw = w + 4 + 3 * k;
-  const uint32_t xw = pw[0], yw = pw[1], mk = pw[2];
+// product k of an op (K > 0, k < K), given its record words (x terms, y terms, m): its 28 joined columns
+LCV_FN void sop_fan_product(uint64_t col[28], uint32_t xw, uint32_t yw, uint32_t mk, uint32_t k, uint32_t masks,
+                            bool mflag, const SopBase& base) {
   uint32_t Xw[13], Yw[12], X[15], Y[14];
   sop_operand(Xw, xw, (masks >> k) & 1u, base);
   sop_operand(Yw, yw, (masks >> (16 + k)) & 1u, base);
