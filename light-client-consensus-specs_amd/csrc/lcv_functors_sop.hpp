@@ -255,20 +255,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
   if (active) f.epilogue(item, lane, my);
 }
 
-// The fan engine's round loop (lcv_sop_fan.hpp; latency mode): ONE item per block of TEAM x MAXK lanes
-// (lcv_hip_launch_sop_fan sizes it to whole waves), lane k * TEAM + o computes product k of op o, so the
-// ops' product-0 lanes — which also run the reductions and tails — are lanes 0 .. TEAM - 1 of the first
-// wave, whose lockstep orders every tail's reads before any store.  The products' joined columns meet in
-// the op's 28-column LDS accumulator by 64-bit LDS atomic adds (ds_add_u64); the op's tail lane reads the
-// sums and zeroes the accumulator for the next round.  Two block barriers per round: after the products
-// (the sums are complete) and after the stores (the next round reads them).
+// The fan engine's round loop (lcv_sop_fan.hpp; latency mode): ONE item per block of TEAM x MAXK x S lanes
+// (S = LCV_FAN_PARTS, 3 when the products' Karatsuba parts are split; lcv_hip_launch_sop_fan sizes it to
+// whole waves), lane (k S + part) TEAM + o computes part `part` of product k of op o, so the ops'
+// product-0 part-0 lanes — which also run the reductions and tails — are lanes 0 .. TEAM - 1 of the first
+// wave, whose lockstep orders every tail's reads before any store; a round of K products keeps its
+// K x S x TEAM busy lanes in the first waves.  The products' columns meet in the op's 28-column LDS
+// accumulator by 64-bit LDS atomic adds (ds_add_u64); the op's tail lane reads the sums and zeroes the
+// accumulator for the next round.  Two block barriers per round: after the products (the sums are
+// complete) and after the stores (the next round reads them).
+// LCV_FAN_X_TIMING (experiments only): per-phase clock sums of the first and the last wave, printed.
+#ifndef LCV_FAN_X_TIMING
+#define LCV_FAN_X_TIMING 0
+#endif
 template <class F>
-__global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
-  constexpr uint32_t T = F::TEAM, KM = F::MAXK, NT = ((T * KM + 63) / 64) * 64;
+__global__ __launch_bounds__(((F::TEAM * F::MAXK * LCV_FAN_PARTS + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM, KM = F::MAXK, S = LCV_FAN_PARTS, NT = ((T * KM * S + 63) / 64) * 64;
   constexpr uint32_t ITEM_WORDS = (F::LDS_WORDS + 1u) & ~1u;  // 8-byte aligned scratch after the slots
   static_assert(T <= 64, "every op's tail lane in the first wave");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t L = threadIdx.x, k = L / T, o = L % T;
+  const uint32_t L = threadIdx.x, k = L / (S * T), part = (L / T) % S, o = L % T;
   const uint32_t item = blockIdx.x;
   const bool active = k < KM && item < n;
   uint32_t* qp = lds + F::SHARED_WORDS;
@@ -304,16 +310,36 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fa
     return c;
   };
   Rec nx = fetch(0);
+#if LCV_FAN_X_TIMING
+  uint64_t tq[5] = {0, 0, 0, 0, 0}, tp = clock64();
+#define LCV_FAN_T(i) do { const uint64_t tn = clock64(); tq[i] += tn - tp; tp = tn; } while (0)
+#else
+#define LCV_FAN_T(i) ((void)0)
+#endif
   for (uint32_t r = 0; r < R; ++r) {
     const Rec cur = nx;
     if (r + 1 < R) nx = fetch(r + 1);
     const uint32_t h0 = cur.h0, K = h0 & 15u;
+    LCV_FAN_T(0);
     if (active && k < K) {
+#if LCV_FAN_SPLIT
+      int64_t c13[13];
+      lcv::sop_fan_part(c13, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, part, base);
+      const uint32_t at = part == 0 ? 0u : (part == 1 ? 14u : 7u);
+      LCV_UNROLL for (int c = 0; c < 13; ++c)
+        __hip_atomic_fetch_add(acc + at + c, (uint64_t)c13[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (part != 2)
+        LCV_UNROLL for (int c = 0; c < 13; ++c)
+          __hip_atomic_fetch_add(acc + 7 + c, (uint64_t)c13[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
       uint64_t col[28];
       lcv::sop_fan_product(col, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, base);
       LCV_UNROLL for (int c = 0; c < 28; ++c) __hip_atomic_fetch_add(acc + c, col[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     }
+    LCV_FAN_T(1);
     __syncthreads();
+    LCV_FAN_T(2);
     if (L < T && item < n) {  // op o's tail, in the first wave: every read of the round precedes its stores
       uint32_t res[13];
       if (K == 0) {
@@ -328,8 +354,16 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK + 63) / 64) * 64) void k_sop_fa
       lcv::sop_tail_value(v, h0, cur.w, cur.pre, my, lds, ns, res, qp);
       lcv::sop_tail_store(h0, cur.pre, my, io_in, io_out, v);
     }
+    LCV_FAN_T(3);
     __syncthreads();
+    LCV_FAN_T(4);
   }
+#if LCV_FAN_X_TIMING
+  if (item == 0 && (L == 0 || L == NT - 64))
+    printf("fan T=%u KM=%u S=%u R=%u wave=%u: fetch %lu products %lu barrier1 %lu tail %lu barrier2 %lu\n", T, KM, S,
+           R, L / 64, tq[0], tq[1], tq[2], tq[3], tq[4]);
+#endif
+#undef LCV_FAN_T
   if (L < T && item < n) f.epilogue(item, L, my);
 }
 #endif

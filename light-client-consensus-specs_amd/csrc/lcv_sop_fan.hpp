@@ -14,8 +14,23 @@
 // The column sums are the batch engine's exactly (the join is linear and every joined column is a true,
 // non-negative column sum below the op's bound), so every result is the batch engine's bit for bit
 // (tests/test_latency_gpu.py).  Device-only; the host simulation runs the batch engine.
+//
+// Split products (LCV_FAN_SPLIT, the default): a lone wave issues a product's 147 multiply-adds back to
+// back, ~1 us of a ~2.9 us final-exponentiation round (measured by removing them).  So each product's
+// three Karatsuba sub-products go to three lanes (part 0: X0 Y0, 1: X1 Y1, 2: (X0 - X1)(Y1 - Y0), 7 x 7
+// limbs, B = 2^196): 49 signed multiply-adds per lane (28-bit limbs are non-negative int32s, so one
+// v_mad_i64_i32 stream serves all three parts without divergence), added into the op's columns at
+// 0 and 7 (part 0), 14 and 7 (part 1) and 7 (part 2): X Y = P0 + (P0 + P2 + D) B + P2 B^2.  A signed
+// partial sum may wrap in the 64-bit LDS column; the op's complete column is the true non-negative sum.
 #pragma once
 #include "lcv_sop.hpp"
+
+#ifndef LCV_FAN_SPLIT
+#define LCV_FAN_SPLIT 1
+#endif
+#ifndef LCV_FAN_PARTS
+#define LCV_FAN_PARTS (LCV_FAN_SPLIT ? 3u : 1u)
+#endif
 
 namespace lcv {
 
@@ -43,6 +58,34 @@ LCV_FN void sop_fan_product(uint64_t col[28], uint32_t xw, uint32_t yw, uint32_t
   int64_t pd[13];
   sop_kara_mac<true>(p0, p2, pd, X, Y);
   sop_kara_join(col, p0, p2, pd);
+}
+
+// part `part` (0, 1, 2) of product k: its 13 signed columns (placed by the caller, see above)
+LCV_FN void sop_fan_part(int64_t c[13], uint32_t xw, uint32_t yw, uint32_t mk, uint32_t k, uint32_t masks,
+                         bool mflag, uint32_t part, const SopBase& base) {
+  uint32_t Xw[13], Yw[12], X[15], Y[14];
+  sop_operand(Xw, xw, (masks >> k) & 1u, base);
+  sop_operand(Yw, yw, (masks >> (16 + k)) & 1u, base);
+  Xw[12] = 0;
+  if (mflag) {  // X *= m (m < 2^16): 13 words
+    uint32_t carry = 0;
+    LCV_UNROLL for (int j = 0; j < 12; ++j) {
+      const uint64_t t = (uint64_t)Xw[j] * mk + carry;
+      Xw[j] = (uint32_t)t;
+      carry = (uint32_t)(t >> 32);
+    }
+    Xw[12] = carry;
+  }
+  sop_to28<12, 14>(Y, Yw);
+  sop_to28<13, 14>(X, Xw);
+  int32_t a[7], b[7];
+  const bool p0 = part == 0, p1 = part == 1;
+  LCV_UNROLL for (int i = 0; i < 7; ++i) {
+    const int32_t xl = (int32_t)X[i], xh = (int32_t)X[i + 7], yl = (int32_t)Y[i], yh = (int32_t)Y[i + 7];
+    a[i] = p0 ? xl : (p1 ? xh : xl - xh);
+    b[i] = p0 ? yl : (p1 ? yh : yh - yl);
+  }
+  sop_mac7s<true>(c, a, b);
 }
 
 }  // namespace lcv

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Per-stage kernel times (HIP events) of ONE update validated through the C ABI, with the latency engine
-(lcv_set_latency_mode(32), opt-in) and with the batch engine (the default) — where the single-call latency of the
-reference-shaped drop-in (sync-protocol.md:512 -> :464) goes.  GPU only."""
+"""Per-stage kernel times (HIP events) of ONE update (and of 16) validated through the C ABI, on the fan engine
+(lcv_set_latency_mode(64), the default for batches of <= 64 rows) and on the batch engine (mode 0) — where the
+single-call latency of the reference-shaped drop-in (sync-protocol.md:512 -> :464) goes.  GPU only.
+LCV_LAT_MODES="64" / LCV_LAT_NS="1" restrict the runs (A/B scripts)."""
 import json
 import os
 import sys
@@ -15,21 +16,23 @@ from lcv.device import Verifier  # noqa: E402
 
 v = Verifier(0)
 out = {}
-for mode in (32, 0):
+modes = [int(x) for x in os.environ.get("LCV_LAT_MODES", "64 0").split()]
+ns = [int(x) for x in os.environ.get("LCV_LAT_NS", "1 16").split()]
+for mode in modes:
     v.set_latency_mode(mode)
-    for n in (1, 16):
+    for n in ns:
         sb = synth.generate(v, n, seed=2)
         v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
         rb = v.upload(sb.updates)
         for _ in range(3):
             v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root)
         ts, st = [], {}
-        for _ in range(10):
+        for _ in range(int(os.environ.get("LCV_LAT_REPS", "10"))):
             t0 = time.perf_counter()
             ok, _ = v.validate_resident(rb, sb.current_slot, sb.genesis_validators_root)
             ts.append(1000 * (time.perf_counter() - t0))
             for k, ms in v.last_timings().items():
-                st[k] = st.get(k, 0.0) + ms / 10
+                st[k] = st.get(k, 0.0) + ms / int(os.environ.get("LCV_LAT_REPS", "10"))
         out[f"{'latency' if mode else 'batch'}_engine_n{n}"] = {
             "wall_ms_median": round(sorted(ts)[len(ts) // 2], 3), "all_valid": bool(ok.all()),
             "stage_ms": {k: round(x, 3) for k, x in st.items() if x > 0}}
