@@ -12,6 +12,13 @@
 #if defined(LCV_KERNEL_UNIT)
 #include "lcv_sop_fan.hpp"
 #endif
+// the fan engine's lanes per product (lcv_sop_fan.hpp; also known to lcv_launch.hpp): 3 = Karatsuba parts split
+#ifndef LCV_FAN_SPLIT
+#define LCV_FAN_SPLIT 1
+#endif
+#ifndef LCV_FAN_PARTS
+#define LCV_FAN_PARTS (LCV_FAN_SPLIT ? 3u : 1u)
+#endif
 
 enum { SOP_LINE_VALS = 6 * LCV_SOP_LINES_NSTEPS, SOP_LINE_WORDS = 2 * SOP_LINE_VALS * 12 };
 // W.lines: item i's two pairings' line values (pairing k at + k * SOP_LINE_VALS * 12 words)
@@ -29,6 +36,7 @@ struct F_sop_lines {
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_LINES_MAXK;  // the fan engine's lanes per op
+  static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;    // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_LINES_NCONST * 12;
   // pairing k of update i: k = 0 e(PK_agg, H(m)), k = 1 e(-G1, signature)
@@ -101,6 +109,7 @@ struct F_sop_acc {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_MILLER_ACC_MAXK;  // the fan engine's lanes per op
+  static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;         // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_MILLER_ACC_NCONST * 12;
   static_assert(LCV_SOP_MILLER_ACC_SLOT_F0_0 == 0 && LCV_SOP_MILLER_ACC_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -124,10 +133,96 @@ struct F_sop_acc {
   }
 };
 
+// Latency mode's Miller loop as one program (tools/gen_sop.py miller_program): both pairings' walks
+// (slots m_* for e(PK_agg, H(m)), s_* for e(-G1, signature) with its G2 subgroup check) beside the
+// accumulation, one step behind, the lines passing through LDS; fan engine only (one update per block,
+// one lane per product: its K = 7 accumulation rounds would fill 11 waves with split products)
+struct F_sop_miller {
+  Work W; SopView P;
+  static constexpr uint32_t MAXK = LCV_SOP_MILLER_MAXK;
+  static constexpr uint32_t FAN_PARTS = 1;
+  static constexpr uint32_t TEAM = LCV_SOP_MILLER_TEAM, LDS_WORDS = LCV_SOP_MILLER_SLOTS * 12 + SOP_PITCH_PAD,
+                            SHARED_WORDS = LCV_SOP_MILLER_NCONST * 12;
+  static_assert(LCV_SOP_MILLER_SLOT_F0_0 == 0 && LCV_SOP_MILLER_SLOT_F5_1 == 11, "f in slots 0..11");
+  LCV_HD const uint32_t* io_in(uint32_t) const { return nullptr; }
+  LCV_HD uint32_t* io_out(uint32_t) const { return nullptr; }
+  // 36 values: each walk's Q, T = (Q, 1) and (-xP, yP) as F_sop_lines' prologue, then f = 1
+  LCV_HD void prologue(uint32_t i, uint32_t lane, uint32_t* lds) const {
+    constexpr uint32_t QS[2][4] = {{LCV_SOP_MILLER_SLOT_M_QX0, LCV_SOP_MILLER_SLOT_M_QX1, LCV_SOP_MILLER_SLOT_M_QY0,
+                                    LCV_SOP_MILLER_SLOT_M_QY1},
+                                   {LCV_SOP_MILLER_SLOT_S_QX0, LCV_SOP_MILLER_SLOT_S_QX1, LCV_SOP_MILLER_SLOT_S_QY0,
+                                    LCV_SOP_MILLER_SLOT_S_QY1}};
+    constexpr uint32_t TS[2][6] = {{LCV_SOP_MILLER_SLOT_M_TX0, LCV_SOP_MILLER_SLOT_M_TX1, LCV_SOP_MILLER_SLOT_M_TY0,
+                                    LCV_SOP_MILLER_SLOT_M_TY1, LCV_SOP_MILLER_SLOT_M_TZ0, LCV_SOP_MILLER_SLOT_M_TZ1},
+                                   {LCV_SOP_MILLER_SLOT_S_TX0, LCV_SOP_MILLER_SLOT_S_TX1, LCV_SOP_MILLER_SLOT_S_TY0,
+                                    LCV_SOP_MILLER_SLOT_S_TY1, LCV_SOP_MILLER_SLOT_S_TZ0, LCV_SOP_MILLER_SLOT_S_TZ1}};
+    constexpr uint32_t PS[2][2] = {{LCV_SOP_MILLER_SLOT_M_NXP, LCV_SOP_MILLER_SLOT_M_YP},
+                                   {LCV_SOP_MILLER_SLOT_S_NXP, LCV_SOP_MILLER_SLOT_S_YP}};
+    for (uint32_t u = lane; u < 36; u += TEAM) {
+      fp x;
+      uint32_t slot;
+      if (u < 24) {
+        const uint32_t k = u / 12, v = u % 12;
+        const bool id = k == 0 ? W.qh_inf[i] != 0 : W.sig_status[i] != PT_OK;
+        if (v < 8) {
+          const uint32_t c = v & 3u;
+          if (id) {
+            fp2 g;
+            if (c < 2) LCV_FP2_SET(g, LCV_G2X);
+            else LCV_FP2_SET(g, LCV_G2Y);
+            x = (c & 1u) ? g.c1 : g.c0;
+          } else {
+            soa_ld_fp(x, k == 0 ? W.qh : W.qs, W.cap, i, c);
+          }
+          slot = v < 4 ? QS[k][c] : TS[k][c];
+        } else if (v < 10) {
+          if (v == 8) fp_one(x);
+          else fp_zero(x);
+          slot = TS[k][v - 4];
+        } else {
+          if (k == 0) {
+            soa_ld_fp(x, W.pk, W.cap, i, v - 10);
+            if (v == 10) fp_neg(x, x);
+          } else if (v == 10) {
+            LCV_FP_SET(x, LCV_G1X_INIT);
+            fp_neg(x, x);
+          } else {
+            LCV_FP_SET(x, LCV_G1NEGY_INIT);
+          }
+          if (id) fp_zero(x);
+          slot = PS[k][v - 10];
+        }
+      } else {
+        slot = u - 24;  // f = 1
+        if (slot == 0) fp_one(x);
+        else fp_zero(x);
+      }
+      LCV_UNROLL for (int j = 0; j < 12; ++j) lds[12 * slot + j] = x.v[j];
+    }
+  }
+  // f -> W.f (as F_sop_acc), and the signature's G2 subgroup check (as F_sop_lines)
+  LCV_HD void epilogue(uint32_t i, uint32_t lane, const uint32_t* lds) const {
+    for (uint32_t s = lane; s < 12; s += TEAM) {
+      uint32_t x[12];
+      LCV_UNROLL for (int j = 0; j < 12; ++j) x[j] = lds[12 * s + j];
+      f12_st_coeff(W.f, i, s, x);
+    }
+    if (lane != 0 || W.sig_status[i] != PT_OK) return;
+    uint32_t e = 0, z = 0;
+    for (int j = 0; j < 12; ++j) {
+      e |= lds[12 * LCV_SOP_MILLER_SLOT_S_E10 + j] | lds[12 * LCV_SOP_MILLER_SLOT_S_E11 + j] |
+           lds[12 * LCV_SOP_MILLER_SLOT_S_E20 + j] | lds[12 * LCV_SOP_MILLER_SLOT_S_E21 + j];
+      z |= lds[12 * LCV_SOP_MILLER_SLOT_S_TZ0 + j] | lds[12 * LCV_SOP_MILLER_SLOT_S_TZ1 + j];
+    }
+    if (e != 0 || z == 0) W.sig_status[i] = PT_BAD;
+  }
+};
+
 struct F_sop_fexp {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_FEXP_MAXK;  // the fan engine's lanes per op
+  static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;   // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_FEXP_NCONST * 12;
   static_assert(LCV_SOP_FEXP_SLOT_F0_0 == 0 && LCV_SOP_FEXP_SLOT_F5_1 == 11, "f in slots 0..11");
@@ -173,6 +268,7 @@ struct F_sop_h2c {
   Work W; SopView P;
   static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_H2C_MAXK;  // the fan engine's lanes per op
+  static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;  // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + SOP_PITCH_PAD,
                             SHARED_WORDS = LCV_SOP_H2C_NCONST * 12;
   static_assert(LCV_SOP_H2C_SLOT_M0X0 == 0 && LCV_SOP_H2C_SLOT_M1Y1 == 7, "SSWU points in slots 0..7");
@@ -269,10 +365,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
 #define LCV_FAN_X_TIMING 0
 #endif
 template <class F>
-__global__ __launch_bounds__(((F::TEAM * F::MAXK * LCV_FAN_PARTS + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
-  constexpr uint32_t T = F::TEAM, KM = F::MAXK, S = LCV_FAN_PARTS, NT = ((T * KM * S + 63) / 64) * 64;
+__global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM, KM = F::MAXK, S = F::FAN_PARTS, NT = ((T * KM * S + 63) / 64) * 64;
   constexpr uint32_t ITEM_WORDS = (F::LDS_WORDS + 1u) & ~1u;  // 8-byte aligned scratch after the slots
   static_assert(T <= 64, "every op's tail lane in the first wave");
+  static_assert(S == 1 || S == 3, "one lane per product, or one per Karatsuba part");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t L = threadIdx.x, k = L / (S * T), part = (L / T) % S, o = L % T;
   const uint32_t item = blockIdx.x;
@@ -322,7 +419,7 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * LCV_FAN_PARTS + 63) / 64) * 6
     const uint32_t h0 = cur.h0, K = h0 & 15u;
     LCV_FAN_T(0);
     if (active && k < K) {
-#if LCV_FAN_SPLIT
+      if constexpr (S == 3) {
       int64_t c13[13];
       lcv::sop_fan_part(c13, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, part, base);
       const uint32_t at = part == 0 ? 0u : (part == 1 ? 14u : 7u);
@@ -331,11 +428,11 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * LCV_FAN_PARTS + 63) / 64) * 6
       if (part != 2)
         LCV_UNROLL for (int c = 0; c < 13; ++c)
           __hip_atomic_fetch_add(acc + 7 + c, (uint64_t)c13[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
+      } else {
       uint64_t col[28];
       lcv::sop_fan_product(col, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, base);
       LCV_UNROLL for (int c = 0; c < 28; ++c) __hip_atomic_fetch_add(acc + c, col[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
+      }
     }
     LCV_FAN_T(1);
     __syncthreads();

@@ -64,11 +64,11 @@ template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStre
   hipLaunchKernelGGL(k_sop<F>, dim3(blocks), dim3(64), lds_bytes, s, f, n, g);
   return hipGetLastError();
 }
-// the fan engine (latency mode, lcv_sop_fan.hpp): one item per block of TEAM x MAXK x LCV_FAN_PARTS lanes
+// the fan engine (latency mode, lcv_sop_fan.hpp): one item per block of TEAM x MAXK x F::FAN_PARTS lanes
 // (whole waves)
 template <class F> __global__ void k_sop_fan(F f, uint32_t n);
 template <class F> hipError_t lcv_hip_launch_sop_fan(const F& f, uint32_t n, hipStream_t s) {
-  constexpr uint32_t NT = ((F::TEAM * F::MAXK * LCV_FAN_PARTS + 63) / 64) * 64;
+  constexpr uint32_t NT = ((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64;
   const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + LCV_SOP_QP_WORDS + ((F::LDS_WORDS + 1u) & ~1u)) +
                            8 * (size_t)F::TEAM * 28;
   hipLaunchKernelGGL(k_sop_fan<F>, dim3(n), dim3(NT), lds_bytes, s, f, n);

@@ -27,6 +27,7 @@ def test_sop_programs_match_oracle():
     for p in progs:
         p.finalize()
     GS.check_miller(progs[0], progs[1])
+    GS.check_miller_fused(progs[0], progs[1], progs[4])  # latency mode's walks + accumulation in one program
     GS.check_fexp(progs[2])
     GS.check_h2c(progs[3])
     text = open(os.path.join(H.PKG, "csrc", "lcv_sop_programs.inc")).read()
@@ -58,7 +59,7 @@ def test_opcount_every_stage():
     # the SOP programs' products and reductions are what the op counter sees (padding products excluded):
     # each is half of a reduced Fp multiplication
     import gen_sop as GS
-    lp, ap, fp, _ = GS.build()
+    lp, ap, fp = GS.build()[:3]
     for p in (lp, ap, fp):
         p.finalize()  # the negated-shadow pass may add a first round
 

@@ -718,14 +718,25 @@ def _psi_consts():
     return inv2(_fp2_pow((1, 1), (P - 1) // 3)), inv2(_fp2_pow((1, 1), (P - 1) // 2))
 
 
-def line_program(team=10):
+def line_program(team=10, p=None, prefix="", rnd=None, line_op=None):
     """One pairing's T walk over |x| (63 doublings, 5 additions; the projective doubling of
     the projective line doubling scaled by 4, no halvings), emitting per step the sparse line
-    (a, b, c) = (c00, c01 * (-xP), c11 * yP), 6 Fp values, io index 6 * step + j."""
-    p = Program("lines", team)
-    qx, qy = slots2(p, "qx"), slots2(p, "qy")
-    nxP, yP = T(p.alloc("nxp")), T(p.alloc("yp"))
-    X, Y, Z = slots2(p, "tx"), slots2(p, "ty"), slots2(p, "tz")
+    (a, b, c) = (c00, c01 * (-xP), c11 * yP), 6 Fp values, io index 6 * step + j.
+    Fused use (miller_program): the walk's slots are allocated on the given Program `p` under names
+    prefix + ..., its rounds go to rnd(ops, step) (step: the Miller step whose line the round computes; -1
+    before the walk, nsteps after it) instead of p.round, line value j of a step is the op
+    line_op(step, j, prods, adds) instead of an emit, and no slot is released (the walks' rounds are
+    interleaved with other rounds afterwards)."""
+    fused = p is not None
+    if p is None:
+        p = Program("lines", team)
+    if rnd is None:
+        rnd = lambda ops, st: p.round(ops)  # noqa: E731
+    if line_op is None:
+        line_op = lambda st, j, prods, adds: Op(None, prods, adds, emit=6 * st + j)  # noqa: E731
+    qx, qy = slots2(p, prefix + "qx"), slots2(p, prefix + "qy")
+    nxP, yP = T(p.alloc(prefix + "nxp")), T(p.alloc(prefix + "yp"))
+    X, Y, Z = slots2(p, prefix + "tx"), slots2(p, prefix + "ty"), slots2(p, prefix + "tz")
     B, Cp, J, XY, YZ = (slots2(p) for _ in range(5))
     BmF, BpF = slots2(p), slots2(p)
     C48 = slots2(p)  # 48 C': carries most of 1728 = 36 * 48, so no scaled operand of the T update needs a 15th limb
@@ -738,28 +749,28 @@ def line_program(team=10):
     # T = [|x|]Q = -[x]Q, so Q is in G2 iff Z != 0, e1 = px Z - X = 0 and e2 = py Z + Y = 0.  The walk's
     # formulas are exact on G2; on a non-member any exceptional case leaves Z = 0 for good (T = Q in an
     # addition gives (0 : 0 : 0), T = -Q gives O, and O stays O), so a non-member is never accepted.
-    px, py = slots2(p, "px"), slots2(p, "py")
+    px, py = slots2(p, prefix + "px"), slots2(p, prefix + "py")
     cx = (T(p.const(PSI_CX[0])), T(p.const(PSI_CX[1])))
     cy = (T(p.const(PSI_CY[0])), T(p.const(PSI_CY[1])))
-    p.round([Op(dst_of(px[c]), fp2_prod((qx[0], ~qx[1]), cx, c)) for c in range(2)] +
-            [Op(dst_of(py[c]), fp2_prod((qy[0], ~qy[1]), cy, c)) for c in range(2)])
+    rnd([Op(dst_of(px[c]), fp2_prod((qx[0], ~qx[1]), cx, c)) for c in range(2)] +
+        [Op(dst_of(py[c]), fp2_prod((qy[0], ~qy[1]), cy, c)) for c in range(2)], -1)
     step = 0
 
     for bit in bin(X_ABS)[3:]:
         # ---- doubling
-        p.round([Op(dst_of(B[c]), fp2_sqr(Y, c)) for c in range(2)] +
-                [Op(dst_of(Cp[c]), fp2_sqr(Z, c, xi=True)) for c in range(2)] +
-                [Op(dst_of(J[c]), fp2_sqr(X, c)) for c in range(2)] +
-                [Op(dst_of(XY[c]), fp2_prod(X, Y, c)) for c in range(2)] +
-                [Op(dst_of(YZ[c]), fp2_prod(Y, Z, c)) for c in range(2)])
+        rnd([Op(dst_of(B[c]), fp2_sqr(Y, c)) for c in range(2)] +
+            [Op(dst_of(Cp[c]), fp2_sqr(Z, c, xi=True)) for c in range(2)] +
+            [Op(dst_of(J[c]), fp2_sqr(X, c)) for c in range(2)] +
+            [Op(dst_of(XY[c]), fp2_prod(X, Y, c)) for c in range(2)] +
+            [Op(dst_of(YZ[c]), fp2_prod(Y, Z, c)) for c in range(2)], step)
         # line: a = B - 12 C', b = 3 J * nxP, c = 2 YZ * yP ;  B -+ 3E with E = 12 C'.  This round holds
         # only the add-in combinations (no products: one REDC of cost); b and c, single products of
         # round-one values, ride in the next round's idle lanes (it has 6 ops of K = 2 on 10 lanes)
         ops = [Op(dst_of(BmF[c]), [], [(B[c].slot, 1), (Cp[c].slot, -36)]) for c in range(2)]
         ops += [Op(dst_of(BpF[c]), [], [(B[c].slot, 1), (Cp[c].slot, 36)]) for c in range(2)]
-        ops += [Op(None, [], [(B[c].slot, 1), (Cp[c].slot, -12)], emit=6 * step + c) for c in range(2)]
+        ops += [line_op(step, c, [], [(B[c].slot, 1), (Cp[c].slot, -12)]) for c in range(2)]
         ops += [Op(dst_of(C48[c]), [], [(Cp[c].slot, 48)]) for c in range(2)]
-        p.round(ops)
+        rnd(ops, step)
         # T: X = 2 XY (B - 3E), Y = (B + 3E)^2 - 1728 C'^2, Z = 8 B YZ, with 1728 C'^2 taken as
         # 36 (48 C0 + 48 C1)(C0 - C1) + 72 (48 C0) C1 u: the scaled operands stay below 2^392 (14 limbs,
         # Karatsuba), where m = 1728 / 3456 on C' itself needed a 15th limb and schoolbook products
@@ -767,55 +778,64 @@ def line_program(team=10):
         ops = [Op(dst_of(X[c]), fp2_prod(XY, BmF, c, m=2)) for c in range(2)]
         ops += [Op(dst_of(Y[c]), fp2_sqr(BpF, c) + ysq[c]) for c in range(2)]
         ops += [Op(dst_of(Z[c]), fp2_prod(B, YZ, c, m=8)) for c in range(2)]
-        ops += [Op(None, [([J[c]], [nxP], 3)], emit=6 * step + 2 + c) for c in range(2)]
-        ops += [Op(None, [([YZ[c]], [yP], 2)], emit=6 * step + 4 + c) for c in range(2)]
-        p.round(ops)
+        ops += [line_op(step, 2 + c, [([J[c]], [nxP], 3)], []) for c in range(2)]
+        ops += [line_op(step, 4 + c, [([YZ[c]], [yP], 2)], []) for c in range(2)]
+        rnd(ops, step)
         step += 1
         if bit == "1":
             # ---- addition T + Q: theta = Y - qy Z, lam = X - qx Z
             # (Z on the x side: the negated reads fall on the walk's running value, Q needs no shadows)
             ops = [Op(dst_of(th[c]), fp2_prod(Z, qy, c, m=-1), [(Y[c].slot, 1)]) for c in range(2)]
             ops += [Op(dst_of(lam[c]), fp2_prod(Z, qx, c, m=-1), [(X[c].slot, 1)]) for c in range(2)]
-            p.round(ops)
+            rnd(ops, step)
             # C = theta^2, D = lam^2; line (theta qx - lam qy, theta * nxP, lam * yP)
             ops = [Op(dst_of(Cc[c]), fp2_sqr(th, c)) for c in range(2)]
             ops += [Op(dst_of(D[c]), fp2_sqr(lam, c)) for c in range(2)]
-            ops += [Op(None, fp2_prod(th, qx, c) + fp2_prod(lam, qy, c, m=-1), emit=6 * step + c)
-                    for c in range(2)]
-            ops += [Op(None, [([th[c]], [nxP], 1)], emit=6 * step + 2 + c) for c in range(2)]
-            ops += [Op(None, [([lam[c]], [yP], 1)], emit=6 * step + 4 + c) for c in range(2)]
-            p.round(ops)
+            ops += [line_op(step, c, fp2_prod(th, qx, c) + fp2_prod(lam, qy, c, m=-1), []) for c in range(2)]
+            ops += [line_op(step, 2 + c, [([th[c]], [nxP], 1)], []) for c in range(2)]
+            ops += [line_op(step, 4 + c, [([lam[c]], [yP], 1)], []) for c in range(2)]
+            rnd(ops, step)
             # E = lam D, F = Z C, G = X D
             ops = [Op(dst_of(E[c]), fp2_prod(lam, D, c)) for c in range(2)]
             ops += [Op(dst_of(F[c]), fp2_prod(Z, Cc, c)) for c in range(2)]
             ops += [Op(dst_of(G[c]), fp2_prod(X, D, c)) for c in range(2)]
-            p.round(ops)
+            rnd(ops, step)
             # H = E + F - 2G ; G - H = 3G - E - F   (third terms as products with the constant 1)
             ops = [Op(dst_of(H[c]), [([G[c]], [one], -2)], [(E[c].slot, 1), (F[c].slot, 1)]) for c in range(2)]
             ops += [Op(dst_of(GmH[c]), [([F[c]], [one], -1)], [(G[c].slot, 3), (E[c].slot, -1)]) for c in range(2)]
-            p.round(ops)
+            rnd(ops, step)
             # X = lam H, Y = theta (G - H) - Y E, Z = Z E
             ops = [Op(dst_of(X[c]), fp2_prod(lam, H, c)) for c in range(2)]
             ops += [Op(dst_of(Y[c]), fp2_prod(th, GmH, c) + fp2_prod(Y, E, c, m=-1)) for c in range(2)]
             ops += [Op(dst_of(Z[c]), fp2_prod(Z, E, c)) for c in range(2)]
-            p.round(ops)
+            rnd(ops, step)
             step += 1
-    p.release([v.slot for f2 in (B, Cp, J, XY, YZ, BmF, BpF, C48, H, GmH) for v in f2])
-    e1, e2 = slots2(p, "e1"), slots2(p, "e2")
-    p.round([Op(dst_of(e1[c]), fp2_prod(Z, px, c), [(X[c].slot, -1)]) for c in range(2)] +
-            [Op(dst_of(e2[c]), fp2_prod(Z, py, c), [(Y[c].slot, 1)]) for c in range(2)])
+    if not fused:
+        p.release([v.slot for f2 in (B, Cp, J, XY, YZ, BmF, BpF, C48, H, GmH) for v in f2])
+    e1, e2 = slots2(p, prefix + "e1"), slots2(p, prefix + "e2")
+    rnd([Op(dst_of(e1[c]), fp2_prod(Z, px, c), [(X[c].slot, -1)]) for c in range(2)] +
+        [Op(dst_of(e2[c]), fp2_prod(Z, py, c), [(Y[c].slot, 1)]) for c in range(2)], step)
     p.nsteps = step
     return p
 
 
-def acc_program(team=12, nsteps=68):
+def acc_program(team=12, nsteps=68, p=None, lines_of=None, rnd=None):
     """Accumulate f <- f^2 * L1(step) * L2(step) over the Miller steps (no squaring in the first and
     in the addition steps, which follow their doubling step in the same loop iteration), then f^x = conj.
     Lines stream in from the line programs' outputs: io index (6 * step + j) for pairing 1 and
-    (6 * nsteps + 6 * step + j) for pairing 2, side-loaded into L1/L2 slots one round ahead."""
-    p = Program("miller_acc", team)
+    (6 * nsteps + 6 * step + j) for pairing 2, side-loaded into L1/L2 slots one round ahead.
+    Fused use (miller_program): f on the given Program `p` (named f...), the lines of step s already in
+    the slots lines_of(s) (written by the walks' rounds: no side-loads, so the first and the addition
+    steps' identity rounds, which only carried the loads, are left out), rounds to rnd(ops, step)."""
+    fused = p is not None
+    if p is None:
+        p = Program("miller_acc", team)
+    if rnd is None:
+        rnd = lambda ops, st: p.round(ops)  # noqa: E731
     f = fp12_slots(p, "f")
-    L = [[slots2(p) for _ in range(3)] for _ in range(2)]   # two lines: (a, b, c)
+    if not fused:
+        L = [[slots2(p) for _ in range(3)] for _ in range(2)]   # two lines: (a, b, c)
+        lines_of = lambda s: L  # noqa: E731
     # step kinds in loop order (dbl, then add when the bit is 1)
     kinds = []
     for bit in bin(X_ABS)[3:]:
@@ -825,6 +845,8 @@ def acc_program(team=12, nsteps=68):
     assert len(kinds) == nsteps
 
     def loads(step):
+        if fused:
+            return [None] * 12
         ops = []
         for k in range(2):
             for j in range(3):
@@ -835,23 +857,68 @@ def acc_program(team=12, nsteps=68):
     first = True
     for s, kind in enumerate(kinds):
         ld = loads(s)
+        Ls = lines_of(s)
         if first:
             # f = 1 (set by the prologue): load both lines, then f = L1 * L2 via two sparse products
-            p.round([Op(dst_of(f[0][0]), [], [(f[0][0].slot, 1)], load=ld[0])] +
-                    [Op(dst_of(f[i // 2][i % 2]), [], [(f[i // 2][i % 2].slot, 1)], load=ld[i]) for i in range(1, 12)])
+            if not fused:
+                rnd([Op(dst_of(f[0][0]), [], [(f[0][0].slot, 1)], load=ld[0])] +
+                    [Op(dst_of(f[i // 2][i % 2]), [], [(f[i // 2][i % 2].slot, 1)], load=ld[i]) for i in range(1, 12)], s)
             first = False
         elif kind == "dbl":
             ops = fp12_sqr_ops(f, f)
             for i, o in enumerate(ops):
                 o.load = ld[i]
-            p.round(ops)
-        else:
+            rnd(ops, s)
+        elif not fused:
             # addition step: no squaring; the loads ride on an identity round
-            p.round([Op(dst_of(f[i // 2][i % 2]), [], [(f[i // 2][i % 2].slot, 1)], load=ld[i]) for i in range(12)])
-        p.round(fp12_mul_line_ops(f, L[0], f))
-        p.round(fp12_mul_line_ops(f, L[1], f))
+            rnd([Op(dst_of(f[i // 2][i % 2]), [], [(f[i // 2][i % 2].slot, 1)], load=ld[i]) for i in range(12)], s)
+        rnd(fp12_mul_line_ops(f, Ls[0], f), s)
+        rnd(fp12_mul_line_ops(f, Ls[1], f), s)
     # x < 0: f -> conj(f)
-    p.round(copy_ops(flat12(conj12(f)), flat12(f)))
+    rnd(copy_ops(flat12(conj12(f)), flat12(f)), nsteps)
+    return p
+
+
+def miller_program(team=32):
+    """Latency mode's Miller loop as ONE program (the fan engine runs it one update per block): both
+    pairings' T walks (line_program, slots m_* for e(PK, H(m)) and s_* for e(-G1, sig), the latter with
+    its G2 subgroup check) and the accumulation (acc_program), the accumulation one step behind the walks
+    in the same rounds: block s holds the walks' rounds of step s + 1 beside the accumulation's rounds of
+    step s, whose lines the walks wrote in block s - 1 into the LDS slots of buffer s mod 2 (no line
+    stream).  ~220 rounds instead of the walk's 217 followed by the accumulation's 205.  The emulation
+    (check_miller_fused) must equal the separate programs' f and subgroup verdicts."""
+    p = Program("miller", team)
+    acc_rounds, walk_rounds = {}, [{}, {}]
+
+    def rec(store):
+        return lambda ops, st: store.setdefault(st, []).append(ops)
+    nst = 68
+    Lb = []  # [buffer][pairing][a b c]: allocated after f (slots 0..11, as in the separate accumulation)
+
+    def lines_of(s):
+        if not Lb:
+            Lb.extend([[[slots2(p) for _ in range(3)] for _ in range(2)] for _ in range(2)])
+        return Lb[s % 2]
+    acc_program(nsteps=nst, p=p, lines_of=lines_of, rnd=rec(acc_rounds))
+
+    def line_op(k):
+        return lambda st, j, prods, adds: Op(dst_of(Lb[st % 2][k][j // 2][j % 2]), prods, adds)
+    for k, prefix in ((0, "m_"), (1, "s_")):
+        lp = line_program(p=p, prefix=prefix, rnd=rec(walk_rounds[k]), line_op=line_op(k))
+        assert lp.nsteps == nst
+    p.nsteps = nst
+
+    def zipped(*seqs):
+        for i in range(max(len(q) for q in seqs)):
+            ops = []
+            for q in seqs:
+                if i < len(q):
+                    ops += q[i]
+            p.round(ops)
+    zipped(walk_rounds[0][-1] + walk_rounds[0][0], walk_rounds[1][-1] + walk_rounds[1][0])
+    for s in range(nst):
+        zipped(walk_rounds[0][s + 1], walk_rounds[1][s + 1], acc_rounds.get(s, []))
+    zipped(acc_rounds[nst])
     return p
 
 
@@ -1429,6 +1496,40 @@ def check_miller(lp, ap):
           f"({len(cases)} points, incl. small-order / G2 + torsion points)")
 
 
+def run_miller_fused(mp, Pp, Q):
+    """Emulate the fused program (miller_program): m_ walk = pairing 0, s_ walk = pairing 1; returns the
+    Fp12 coefficients and the signature walk's subgroup verdict."""
+    mem = {s: 0 for s in range(mp.nslots)}
+    for k, prefix in ((0, "m_"), (1, "s_")):
+        (qx0, qx1), (qy0, qy1) = Q[k]
+        pt = Pp[k]
+        for nm, v in (("qx0", qx0), ("qx1", qx1), ("qy0", qy0), ("qy1", qy1), ("tx0", qx0), ("tx1", qx1),
+                      ("ty0", qy0), ("ty1", qy1), ("tz0", 1), ("tz1", 0), ("nxp", (-pt[0]) % P), ("yp", pt[1])):
+            mem[mp.named[prefix + nm]] = mont(v)
+    mem[mp.named["f0_0"]] = mont(1)
+    mp.emulate(mem)
+    e = [mem[mp.named["s_" + k]] for k in ("e10", "e11", "e20", "e21")]
+    z = [mem[mp.named["s_" + k]] for k in ("tz0", "tz1")]
+    return _f12_from_mem(mp, mem, "f"), bool(any(z) and not any(e))
+
+
+def check_miller_fused(lp, ap, mp):
+    from oracle import bls12_381 as B
+    rnd = random.Random(17)
+    for _ in range(2):
+        a, b = rnd.randrange(1, 1 << 60), rnd.randrange(1, 1 << 60)
+        Pp = [B.g1_mul(B.G1_GEN, a), B.g1_neg(B.G1_GEN)]
+        Q = [B.g2_mul(B.G2_GEN, b), B.g2_mul(B.G2_GEN, b + 11)]
+        g, ok = run_miller_fused(mp, Pp, Q)
+        assert g == run_miller(lp, ap, Pp, Q), "fused Miller program differs from lines + accumulation"
+        assert ok, "fused subgroup check rejected a G2 point"
+    bad = B.g2_add(B.g2_mul(B.G2_GEN, 5), B.g2_point_of_order(13))
+    g, ok = run_miller_fused(mp, [B.g1_neg(B.G1_GEN), B.g1_neg(B.G1_GEN)], [B.g2_mul(B.G2_GEN, 3), bad])
+    assert not ok and not B.g2_in_subgroup(bad), "fused subgroup check accepted a non-member"
+    print("  SOP fused Miller program (both walks beside the accumulation) equals lines + accumulation; "
+          "its subgroup check rejects a G2 + torsion point")
+
+
 def check_fexp(fp):
     from oracle import bls12_381 as B
     rnd = random.Random(9)
@@ -1490,7 +1591,8 @@ def build():
     ap = acc_program(nsteps=lp.nsteps)
     fp = fexp_program()
     hp = h2c_program()
-    progs = (lp, ap, fp, hp)
+    mp = miller_program()
+    progs = (lp, ap, fp, hp, mp)
     perms = os.environ.get("LCV_SOP_SLOT_PERMS")  # experiment: JSON {program: perm}
     if perms:
         import json
@@ -1513,6 +1615,7 @@ def main():
         print(p.stats())
     if args.check:
         check_miller(progs[0], progs[1])
+        check_miller_fused(progs[0], progs[1], progs[4])
         check_fexp(progs[2])
         check_h2c(progs[3])
     emit(progs, args.out)

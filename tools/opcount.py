@@ -28,6 +28,9 @@ def count(n: int = 8, participation: str = "full", npool: int = 1) -> dict:
     lib = Lib(os.path.join(PKG, "build", "liblcv_hostsim_ops.so"))
     lib.dll.lcv_debug_opcounts.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
     v = Verifier(lib=lib)
+    # the batch engine's pipeline (each stage its own program), as the bench's batches of 10^4 run it; a
+    # few-row batch would otherwise take latency mode's fused Miller program (no separate line stages)
+    v.set_latency_mode(0)
     sb = synth.generate(v, n, seed=2, participation=participation, npool=npool)
     v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     ok, _ = v.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
