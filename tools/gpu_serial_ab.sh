@@ -12,7 +12,7 @@ trap 'cp $OUT/.liblcv_orig.so $LIB' EXIT
 for i in ${ROUNDS:-1 2}; do
   for v in ${VARIANTS:-A B}; do
     cp abp/liblcv_$v.so $LIB &&
-    timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --quick ${BENCH_ARGS:-} \
+    timeout -k 10 200 python -u bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --quick ${BENCH_ARGS:-} \
       > $OUT/b_${v}_$i.json 2> $OUT/b_${v}_$i.err || exit 1
     python -c "
 import json; d=json.load(open('$OUT/b_${v}_$i.json')); s=d['stage_kernel_ms_per_step']
