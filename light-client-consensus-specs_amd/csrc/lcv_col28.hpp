@@ -148,6 +148,23 @@ LCV_FN void sop_redc28(uint32_t r[13], uint64_t col[28]) {
 }
 
 
+// R = 2^392 (fourteen full 28-bit digits): L (14 limbs) = (T + M p) / 2^392, normalised 28-bit limbs, for the
+// limb-form exponentiation chains (lcv_field.hpp fp_pow_lf), whose values never leave 28-bit limbs
+LCV_FN void sop_redc28_392(uint32_t L[14], uint64_t col[28]) {
+  uint64_t carry = 0;
+  LCV_UNROLL for (int i = 0; i < 14; ++i) {
+    const uint64_t v = col[i] + carry;
+    const uint32_t q = ((uint32_t)v * kNP28) & SOP_M28;
+    carry = (v + (uint64_t)q * kP28.v[0]) >> 28;  // the low 28 bits vanish
+    LCV_UNROLL for (int j = 1; j < 14; ++j) col[i + j] += (uint64_t)q * kP28.v[j];
+  }
+  LCV_UNROLL for (int c = 14; c < 28; ++c) {
+    const uint64_t t = col[c] + carry;
+    L[c - 14] = (uint32_t)t & SOP_M28;
+    carry = t >> 28;
+  }
+}
+
 // squaring forms: c = x x over 7 limbs (cross products doubled: 28 multiply-adds) and its signed twin
 template <class A, class L>
 LCV_FN void col_sqr7(A c[13], const L* x) {
@@ -183,6 +200,30 @@ LCV_FN void fp_sqr_c28(uint32_t r[13], const uint32_t a[12]) {
   LCV_UNROLL for (int k = 0; k < 13; ++k) s[k] = -s[k];  // D = (X0 - X1)(X1 - X0) = -(X0 - X1)^2
   sop_kara_join(col, p0, p2, s);
   sop_redc28(r, col);
+}
+
+// limb-form Montgomery square / product with R = 2^392 (values < 2p stay < 2p: (T + M p) / R < 4p^2 / R + p)
+LCV_FN void fp_sqr_lf(uint32_t r[14], const uint32_t a[14]) {
+  int32_t d[7];
+  LCV_UNROLL for (int i = 0; i < 7; ++i) d[i] = (int32_t)(a[i] - a[i + 7]);
+  uint64_t p0[13], p2[13], col[28];
+  int64_t s[13];
+  col_sqr7(p0, a);
+  col_sqr7(p2, a + 7);
+  col_sqr7(s, d);
+  LCV_UNROLL for (int k = 0; k < 13; ++k) s[k] = -s[k];
+  sop_kara_join(col, p0, p2, s);
+  sop_redc28_392(r, col);
+}
+LCV_FN void fp_mul_lf(uint32_t r[14], const uint32_t a[14], const uint32_t b[14]) {
+  uint32_t x[15];
+  LCV_UNROLL for (int i = 0; i < 14; ++i) x[i] = a[i];
+  x[14] = 0;
+  uint64_t p0[13], p2[13], col[28];
+  int64_t pd[13];
+  sop_kara_mac<true>(p0, p2, pd, x, b);
+  sop_kara_join(col, p0, p2, pd);
+  sop_redc28_392(r, col);
 }
 
 }  // namespace lcv

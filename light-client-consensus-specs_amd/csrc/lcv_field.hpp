@@ -350,8 +350,100 @@ LCV_DEF_POW(fp_inv_fermat, LCV_EXP_P_MINUS_2, LCV_EXP_P_MINUS_2_BITS)    // a^(p
     }                                                                                     \
     r = acc;                                                                              \
   }
+// The same window walk on 28-bit limbs with R = 2^392 (lcv_col28.hpp fp_sqr_lf / fp_mul_lf): the operand
+// conversions, the packing of each product into words and its conditional subtraction leave the chain (a
+// limb value < 2p squares to < 2p), so a product is its multiply-adds and quotient chain only.  In: a R ->
+// a 2^392 (one product with the raw constant 2^392 mod p); out: the chain's a^e 2^392 -> a^e R (one product
+// with 2^376) after packing and one subtraction.  Results equal the word-form walk's (both are fully reduced).
+// Used by the latency-mode twins only (lcv_k_lat.hip defines LCV_POW_LF 1): a lone wave's chain runs
+// 1.55 -> 1.14-1.25 ms for the SSWU maps, but at full batches the 28 KB LDS table per block crowds the
+// co-resident final exponentiation (LDS- and VGPR-bound at 12 waves per CU) out of LDS — the serving loop
+// measured 0.5-1 % slower — and the register-table form spilled 624 B per lane (1.2 % slower).
+#ifndef LCV_POW_LF
+#if defined(LCV_HOSTSIM) && !defined(LCV_CPU_FAST)
+#define LCV_POW_LF 1  // the host simulation runs the limb form, so the CPU tests check it against the oracle
+#else
+#define LCV_POW_LF 0
+#endif
+#endif
+#if LCV_POW_LF
+LCV_FN void fp_lf_in(uint32_t L[14], const fp& a) {
+  fp c, t;
+  LCV_FP_SET(c, LCV_2E392_RAW_INIT);
+  fp_mul(t, a, c);
+  sop_to28<12, 14>(L, t.v);
+}
+LCV_FN void fp_lf_out(fp& r, const uint32_t L[14]) {
+  uint32_t w[12];
+  LCV_UNROLL for (int k = 0; k < 12; ++k) {  // word k = bits 32k .. 32k + 31 of the limb string (< 2^382)
+    const int b = 32 * k, j = b / 28, s = b % 28;
+    uint32_t x = L[j] >> s;
+    if (j + 1 < 14) x |= L[j + 1] << (28 - s);
+    if (s > 24 && j + 2 < 14) x |= L[j + 2] << (56 - s);
+    w[k] = x;
+  }
+  fp t, c;
+  fp_reduce_once(t.v, w);
+  LCV_FP_SET(c, LCV_2E376_RAW_INIT);
+  fp_mul(r, t, c);
+}
+// the window table a^1, a^3, .., a^15 (8 x 14 limbs per lane): in LDS on the device — one 28 KB buffer per
+// 64-lane block of a per-item kernel (k_items; every caller of these chains is one), lane-interleaved, read at a
+// wave-uniform index (the exponent is public) — instead of 112 VGPRs and a select chain per window
+#if defined(__HIP_DEVICE_COMPILE__)
+LCV_FN uint32_t* pow_lf_table() {
+  __shared__ uint32_t t[8 * 14 * 64];
+  return t + (threadIdx.x & 63u);
+}
+#define LCV_POW_TAB(k, q) tabp[((k) * 14 + (q)) * 64]
+#define LCV_POW_TAB_DECL uint32_t* tabp = pow_lf_table();
+#else
+#define LCV_POW_TAB(k, q) tabh[k][q]
+#define LCV_POW_TAB_DECL uint32_t tabh[8][14];
+#endif
+#define LCV_DEF_POW_LF(fname, EXPARR, NBITS)                                              \
+  LCV_FN void fname(fp& r, const fp& a_) {                                                \
+    uint32_t a[14], t[14], a2[14], acc[14];                                               \
+    LCV_POW_TAB_DECL                                                                      \
+    fp_lf_in(a, a_);                                                                      \
+    LCV_UNROLL for (int j = 0; j < 14; ++j) LCV_POW_TAB(0, j) = a[j];                     \
+    fp_sqr_lf(a2, a);                                                                     \
+    LCV_UNROLL for (int j = 0; j < 14; ++j) t[j] = a[j];                                  \
+    LCV_NOUNROLL for (int k = 1; k < 8; ++k) {                                            \
+      fp_mul_lf(t, t, a2);                                                                \
+      LCV_UNROLL for (int j = 0; j < 14; ++j) LCV_POW_TAB(k, j) = t[j];                   \
+    }                                                                                     \
+    LCV_UNROLL for (int j = 0; j < 14; ++j) acc[j] = a[j];                                \
+    bool started = false;                                                                 \
+    int i = (NBITS) - 1;                                                                  \
+    LCV_NOUNROLL while (i >= 0) {                                                         \
+      if (!((EXPARR[i >> 5] >> (i & 31)) & 1u)) {                                         \
+        fp_sqr_lf(acc, acc);                                                              \
+        --i;                                                                              \
+        continue;                                                                         \
+      }                                                                                   \
+      int j = i - 3 < 0 ? 0 : i - 3;                                                      \
+      while (!((EXPARR[j >> 5] >> (j & 31)) & 1u)) ++j;                                   \
+      uint32_t w = 0;                                                                     \
+      for (int k = i; k >= j; --k) {                                                      \
+        w = (w << 1) | ((EXPARR[k >> 5] >> (k & 31)) & 1u);                               \
+        if (started) fp_sqr_lf(acc, acc);                                                 \
+      }                                                                                   \
+      uint32_t m[14];                                                                     \
+      LCV_UNROLL for (int q = 0; q < 14; ++q) m[q] = LCV_POW_TAB(w >> 1, q);              \
+      if (started) fp_mul_lf(acc, acc, m);                                                \
+      else LCV_UNROLL for (int q = 0; q < 14; ++q) acc[q] = m[q];                         \
+      started = true;                                                                     \
+      i = j - 1;                                                                          \
+    }                                                                                     \
+    fp_lf_out(r, acc);                                                                    \
+  }
+LCV_DEF_POW_LF(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
+LCV_DEF_POW_LF(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
+#else
 LCV_DEF_POW_W4(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
 LCV_DEF_POW_W4(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
+#endif
 LCV_DEF_POW(fp_pow_pm1d2, LCV_EXP_P_MINUS_1_DIV_2, LCV_EXP_P_MINUS_1_DIV_2_BITS)  // Legendre
 
 // ---- conversions (raw = canonical integer limbs, not Montgomery)

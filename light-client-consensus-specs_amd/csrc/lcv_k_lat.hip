@@ -1,8 +1,10 @@
 // lcv_k_lat.hip — kernel unit: the latency-mode twins F_h2c_map_lat and F_sig_lat (lcv_functors.hpp) of the SSWU
-// maps and the signature decoding, built with the field products inlined (LCV_FP_CALL 0, lcv_common.hpp).
+// maps and the signature decoding, built with the field products inlined (LCV_FP_CALL 0, lcv_common.hpp) and
+// the square-root exponentiations in limb form (LCV_POW_LF 1, lcv_field.hpp).
 #define LCV_KERNEL_UNIT 1
 #define LCV_HD __device__
 #define LCV_FP_CALL 0
+#define LCV_POW_LF 1  // the sqrt chains on 28-bit limbs with the window table in LDS (lcv_field.hpp)
 #include "lcv_launch.hpp"
 #include "lcv_functors.hpp"
 
