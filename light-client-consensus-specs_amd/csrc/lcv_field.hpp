@@ -355,15 +355,18 @@ LCV_DEF_POW(fp_inv_fermat, LCV_EXP_P_MINUS_2, LCV_EXP_P_MINUS_2_BITS)    // a^(p
 // limb value < 2p squares to < 2p), so a product is its multiply-adds and quotient chain only.  In: a R ->
 // a 2^392 (one product with the raw constant 2^392 mod p); out: the chain's a^e 2^392 -> a^e R (one product
 // with 2^376) after packing and one subtraction.  Results equal the word-form walk's (both are fully reduced).
-// Used by the latency-mode twins only (lcv_k_lat.hip defines LCV_POW_LF 1): a lone wave's chain runs
-// 1.55 -> 1.14-1.25 ms for the SSWU maps, but at full batches the 28 KB LDS table per block crowds the
-// co-resident final exponentiation (LDS- and VGPR-bound at 12 waves per CU) out of LDS — the serving loop
-// measured 0.5-1 % slower — and the register-table form spilled 624 B per lane (1.2 % slower).
+// LCV_POW_LF 1 (the latency-mode twins, lcv_k_lat.hip): 4-bit window, table in LDS — a lone wave's SSWU maps
+// 1.55 -> 1.13 ms; at full batches the 28 KB LDS table per block crowds the co-resident final exponentiation
+// (LDS- and VGPR-bound at 12 waves per CU) and the serving loop measured 0.5-1 % slower.  LCV_POW_LF 2 (the
+// batch kernels): 3-bit window, four table entries in registers (the 4-bit register table spilled 624 B per
+// lane): serving loop +1.3 %, one batch at a time -3.7 % (profiles/r05_v5/pow_ab.txt).  0: the word form.
 #ifndef LCV_POW_LF
-#if defined(LCV_HOSTSIM) && !defined(LCV_CPU_FAST)
+#if defined(LCV_CPU_FAST)
+#define LCV_POW_LF 0  // the CPU baseline: its 64-bit limb products beat 28-bit columns on a scalar core
+#elif defined(LCV_HOSTSIM)
 #define LCV_POW_LF 1  // the host simulation runs the limb form, so the CPU tests check it against the oracle
 #else
-#define LCV_POW_LF 0
+#define LCV_POW_LF 2  // batch kernels: limb form, 3-bit window, table in registers
 #endif
 #endif
 #if LCV_POW_LF
@@ -390,16 +393,25 @@ LCV_FN void fp_lf_out(fp& r, const uint32_t L[14]) {
 // the window table a^1, a^3, .., a^15 (8 x 14 limbs per lane): in LDS on the device — one 28 KB buffer per
 // 64-lane block of a per-item kernel (k_items; every caller of these chains is one), lane-interleaved, read at a
 // wave-uniform index (the exponent is public) — instead of 112 VGPRs and a select chain per window
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && LCV_POW_LF == 1
 LCV_FN uint32_t* pow_lf_table() {
   __shared__ uint32_t t[8 * 14 * 64];
   return t + (threadIdx.x & 63u);
 }
+#define LCV_POW_WB 4
 #define LCV_POW_TAB(k, q) tabp[((k) * 14 + (q)) * 64]
 #define LCV_POW_TAB_DECL uint32_t* tabp = pow_lf_table();
+#define LCV_POW_TAB_GET(m, idx) LCV_UNROLL for (int q = 0; q < 14; ++q) m[q] = LCV_POW_TAB(idx, q);
 #else
+// registers (LCV_POW_LF 2: a 3-bit window, four entries, for the batch kernels' register budget; the host
+// simulation: 4 bits); the entry is picked by wave-uniform branches (the exponent is public)
+#define LCV_POW_WB (LCV_POW_LF == 2 ? 3 : 4)
 #define LCV_POW_TAB(k, q) tabh[k][q]
-#define LCV_POW_TAB_DECL uint32_t tabh[8][14];
+#define LCV_POW_TAB_DECL uint32_t tabh[1 << (LCV_POW_WB - 1)][14];
+#define LCV_POW_TAB_GET(m, idx)                                                           \
+  LCV_UNROLL for (int q = 0; q < 14; ++q) m[q] = tabh[0][q];                              \
+  LCV_UNROLL for (int k = 1; k < (1 << (LCV_POW_WB - 1)); ++k)                             \
+    if ((idx) == (uint32_t)k) LCV_UNROLL for (int q = 0; q < 14; ++q) m[q] = tabh[k][q];
 #endif
 #define LCV_DEF_POW_LF(fname, EXPARR, NBITS)                                              \
   LCV_FN void fname(fp& r, const fp& a_) {                                                \
@@ -409,7 +421,7 @@ LCV_FN uint32_t* pow_lf_table() {
     LCV_UNROLL for (int j = 0; j < 14; ++j) LCV_POW_TAB(0, j) = a[j];                     \
     fp_sqr_lf(a2, a);                                                                     \
     LCV_UNROLL for (int j = 0; j < 14; ++j) t[j] = a[j];                                  \
-    LCV_NOUNROLL for (int k = 1; k < 8; ++k) {                                            \
+    LCV_UNROLL for (int k = 1; k < (1 << (LCV_POW_WB - 1)); ++k) {                         \
       fp_mul_lf(t, t, a2);                                                                \
       LCV_UNROLL for (int j = 0; j < 14; ++j) LCV_POW_TAB(k, j) = t[j];                   \
     }                                                                                     \
@@ -422,7 +434,7 @@ LCV_FN uint32_t* pow_lf_table() {
         --i;                                                                              \
         continue;                                                                         \
       }                                                                                   \
-      int j = i - 3 < 0 ? 0 : i - 3;                                                      \
+      int j = i - (LCV_POW_WB - 1) < 0 ? 0 : i - (LCV_POW_WB - 1);                         \
       while (!((EXPARR[j >> 5] >> (j & 31)) & 1u)) ++j;                                   \
       uint32_t w = 0;                                                                     \
       for (int k = i; k >= j; --k) {                                                      \
@@ -430,7 +442,7 @@ LCV_FN uint32_t* pow_lf_table() {
         if (started) fp_sqr_lf(acc, acc);                                                 \
       }                                                                                   \
       uint32_t m[14];                                                                     \
-      LCV_UNROLL for (int q = 0; q < 14; ++q) m[q] = LCV_POW_TAB(w >> 1, q);              \
+      LCV_POW_TAB_GET(m, w >> 1)                                                          \
       if (started) fp_mul_lf(acc, acc, m);                                                \
       else LCV_UNROLL for (int q = 0; q < 14; ++q) acc[q] = m[q];                         \
       started = true;                                                                     \
