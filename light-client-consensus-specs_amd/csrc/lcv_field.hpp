@@ -10,6 +10,7 @@
 #include "lcv_common.hpp"
 #include "lcv_consts.inc"
 #include "lcv_col28.hpp"
+#include "lcv_wave.hpp"
 
 namespace lcv {
 
@@ -450,8 +451,51 @@ LCV_FN uint32_t* pow_lf_table() {
     }                                                                                     \
     fp_lf_out(r, acc);                                                                    \
   }
+#if defined(__HIP_DEVICE_COMPILE__) && LCV_POW_LF == 3
+// LCV_POW_LF 3 (the latency-mode twins, one item per wave): the same window walk with each product spread
+// over the wave (lcv_wave.hpp wv_mul; the 4-bit window table is one register per entry)
+#define LCV_DEF_POW_WAVE(fname, EXPARR, NBITS)                                            \
+  LCV_FN void fname(fp& r, const fp& a_) {                                                \
+    WaveTabs T;                                                                           \
+    wv_tabs(T);                                                                           \
+    uint32_t L[14];                                                                       \
+    fp_lf_in(L, a_);                                                                      \
+    const uint32_t a = wv_scatter(L);                                                     \
+    uint32_t tab[8];                                                                      \
+    tab[0] = a;                                                                           \
+    const uint32_t a2 = wv_mul(a, a, T);                                                  \
+    LCV_UNROLL for (int k = 1; k < 8; ++k) tab[k] = wv_mul(tab[k - 1], a2, T);            \
+    uint32_t acc = a;                                                                     \
+    bool started = false;                                                                 \
+    int i = (NBITS) - 1;                                                                  \
+    LCV_NOUNROLL while (i >= 0) {                                                         \
+      if (!((EXPARR[i >> 5] >> (i & 31)) & 1u)) {                                         \
+        acc = wv_mul(acc, acc, T);                                                        \
+        --i;                                                                              \
+        continue;                                                                         \
+      }                                                                                   \
+      int j = i - 3 < 0 ? 0 : i - 3;                                                      \
+      while (!((EXPARR[j >> 5] >> (j & 31)) & 1u)) ++j;                                   \
+      uint32_t w = 0;                                                                     \
+      for (int k = i; k >= j; --k) {                                                      \
+        w = (w << 1) | ((EXPARR[k >> 5] >> (k & 31)) & 1u);                               \
+        if (started) acc = wv_mul(acc, acc, T);                                           \
+      }                                                                                   \
+      uint32_t m = tab[0];                                                                \
+      LCV_UNROLL for (int k = 1; k < 8; ++k) m = (w >> 1) == (uint32_t)k ? tab[k] : m;     \
+      acc = started ? wv_mul(acc, m, T) : m;                                              \
+      started = true;                                                                     \
+      i = j - 1;                                                                          \
+    }                                                                                     \
+    wv_gather(L, acc);                                                                    \
+    fp_lf_out(r, L);                                                                      \
+  }
+LCV_DEF_POW_WAVE(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
+LCV_DEF_POW_WAVE(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
+#else
 LCV_DEF_POW_LF(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
 LCV_DEF_POW_LF(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
+#endif
 #else
 LCV_DEF_POW_W4(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
 LCV_DEF_POW_W4(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)

@@ -135,6 +135,7 @@ struct F_dbg_pow {  // the sqrt-candidate exponentiations (sliding window, fp_po
     fp_pow_p3d4(r, a); fp_to_be48(o + 48, r);
   }
 };
+struct F_dbg_pow_lat { F_dbg_pow f; LCV_HD void operator()(uint32_t i) const { f(i); } };  // lcv_k_lat.hip's chains
 struct F_export_g2 {  // SoA affine G2 -> canonical bytes
   const uint32_t* base; uint32_t cap; uint8_t* out;
   LCV_HD void operator()(uint32_t i) const {

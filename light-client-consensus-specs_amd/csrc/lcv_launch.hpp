@@ -23,9 +23,20 @@ __global__ __launch_bounds__(64, 1) void k_items(F f, uint32_t n) {
   const uint32_t i = blockIdx.x * 64u + threadIdx.x;
   if (i < n) f(i);
 }
+// LCV_WAVE_ITEMS (lcv_k_lat.hip): one item per 64-lane wave, every lane running it (the wave-cooperative
+// square-root chains, lcv_wave.hpp)
+template <class F>
+__global__ __launch_bounds__(64, 1) void k_wave(F f, uint32_t n) {
+  (void)n;
+  f(blockIdx.x);
+}
 template <class F> hipError_t lcv_hip_launch(const F& f, uint32_t n, hipStream_t s) {
+#if defined(LCV_WAVE_ITEMS)
+  hipLaunchKernelGGL(k_wave<F>, dim3(n), dim3(64), 0, s, f, n);
+#else
   const uint32_t blocks = (n + 63u) / 64u;
   hipLaunchKernelGGL(k_items<F>, dim3(blocks), dim3(64), 0, s, f, n);
+#endif
   return hipGetLastError();
 }
 // Team kernels: F::TEAM lanes cooperate on one item (64 / TEAM items per wave), exchanging values

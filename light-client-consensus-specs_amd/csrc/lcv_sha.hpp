@@ -49,6 +49,34 @@ LCV_FN void sha256_iv(uint32_t st[8]) {
 }
 
 // H(x || y) — SSZ node hash
+#ifndef LCV_SHA_CALL
+#define LCV_SHA_CALL 0
+#endif
+#if LCV_SHA_CALL && defined(__HIP_DEVICE_COMPILE__)
+// LCV_SHA_CALL=1: one out-of-line node hash per kernel (16 scalar words in, 8 out in registers), so a
+// kernel with many hash sites keeps one copy of the two unrolled compressions (register pressure).
+__device__ __noinline__ h256 hash_pair_call(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t x4,
+                                            uint32_t x5, uint32_t x6, uint32_t x7, uint32_t y0, uint32_t y1,
+                                            uint32_t y2, uint32_t y3, uint32_t y4, uint32_t y5, uint32_t y6,
+                                            uint32_t y7) {
+  uint32_t st[8];
+  sha256_iv(st);
+  const uint32_t blk[16] = {x0, x1, x2, x3, x4, x5, x6, x7, y0, y1, y2, y3, y4, y5, y6, y7};
+  sha256_compress(st, blk);
+  uint32_t pad[16];
+  pad[0] = 0x80000000u;
+  LCV_UNROLL for (int i = 1; i < 15; ++i) pad[i] = 0;
+  pad[15] = 512;
+  sha256_compress(st, pad);
+  h256 out;
+  LCV_UNROLL for (int i = 0; i < 8; ++i) out.w[i] = st[i];
+  return out;
+}
+LCV_FN void hash_pair(h256& out, const h256& x, const h256& y) {
+  out = hash_pair_call(x.w[0], x.w[1], x.w[2], x.w[3], x.w[4], x.w[5], x.w[6], x.w[7], y.w[0], y.w[1], y.w[2],
+                       y.w[3], y.w[4], y.w[5], y.w[6], y.w[7]);
+}
+#else
 LCV_FN void hash_pair(h256& out, const h256& x, const h256& y) {
   uint32_t st[8];
   sha256_iv(st);
@@ -62,6 +90,7 @@ LCV_FN void hash_pair(h256& out, const h256& x, const h256& y) {
   sha256_compress(st, pad);
   LCV_UNROLL for (int i = 0; i < 8; ++i) out.w[i] = st[i];
 }
+#endif
 
 LCV_FN void h256_zero(h256& r) { LCV_UNROLL for (int i = 0; i < 8; ++i) r.w[i] = 0; }
 LCV_FN bool h256_is_zero(const h256& a) {

@@ -58,15 +58,23 @@ def _oracle_sig(sig: bytes):
     return (0, pt) if B.g2_in_subgroup(pt) else (2, pt)
 
 
-def test_fp_pow_windowed(gpu_verifier):
-    """fp_pow_p1d4 / fp_pow_p3d4 (sliding window, w = 4) vs pow() on edge and random inputs."""
+@pytest.mark.parametrize("latency_rows", [64, 0])
+def test_fp_pow_windowed(gpu_verifier, latency_rows):
+    """fp_pow_p1d4 / fp_pow_p3d4 (sliding window) vs pow() on edge and random inputs: latency mode (64) runs
+    the latency twins' chains (one value per wave, each product spread over the wave: lcv_wave.hpp), 0 the
+    batch kernels' one-lane chains."""
     rng = random.Random(21)
-    xs = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 4, 5]
+    xs = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 4, 5, (1 << 380) % P, P - (1 << 370)]
     while len(xs) < 40:
         a = rng.randrange(P)
         xs.append(a)
         xs.append(a * a % P)  # a residue
-    out = gpu_verifier.debug_fp_pow(np.frombuffer(b"".join(_be48(x) for x in xs), np.uint8))
+    prev = getattr(gpu_verifier, "latency_mode", 64)
+    gpu_verifier.set_latency_mode(latency_rows)
+    try:
+        out = gpu_verifier.debug_fp_pow(np.frombuffer(b"".join(_be48(x) for x in xs), np.uint8))
+    finally:
+        gpu_verifier.set_latency_mode(prev)
     for i, x in enumerate(xs):
         got = _ints(out[i], 2)
         assert got == [pow(x, (P + 1) // 4, P), pow(x, (P - 3) // 4, P)], x

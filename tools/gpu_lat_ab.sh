@@ -16,6 +16,6 @@ for i in ${ROUNDS:-1 2}; do
       > $OUT/lat_${v}_$i.json 2> $OUT/lat_${v}_$i.err || exit 1
     python -c "
 import json; d=json.load(open('$OUT/lat_${v}_$i.json'))['latency_engine_n1']
-s=d['stage_ms']; print('$v', $i, d['wall_ms_median'], {k: s[k] for k in ('h2c_sswu','hash_to_g2','miller_lines','miller_loop','final_exp') if k in s})"
+s=d['stage_ms']; print('$v', $i, d['wall_ms_median'], {k: s[k] for k in ('nsc_htr','pre_checks','sig_decode','h2c_sswu','hash_to_g2','miller_loop','final_exp') if k in s})"
   done
 done

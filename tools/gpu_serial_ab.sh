@@ -16,6 +16,6 @@ for i in ${ROUNDS:-1 2}; do
       > $OUT/b_${v}_$i.json 2> $OUT/b_${v}_$i.err || exit 1
     python -c "
 import json; d=json.load(open('$OUT/b_${v}_$i.json')); s=d['stage_kernel_ms_per_step']
-print('$v', $i, round(d['value']), d['serial_ms_per_step'], {k: s.get(k) for k in ('miller_loop', 'miller_lines', 'miller_lines_sig', 'final_exp', 'hash_to_g2', 'g1_aggregate')})"
+print('$v', $i, round(d['value']), d['serial_ms_per_step'], {k: s.get(k) for k in (${KEYS:-'miller_loop', 'miller_lines', 'miller_lines_sig', 'final_exp', 'hash_to_g2', 'g1_aggregate'})})"
   done
 done
