@@ -454,7 +454,7 @@ LCV_FN uint32_t* pow_lf_table() {
 #if defined(__HIP_DEVICE_COMPILE__) && LCV_POW_LF == 3
 // LCV_POW_LF 3 (the latency-mode twins, one item per wave): the same window walk with each product spread
 // over the wave (lcv_wave.hpp wv_mul; the 4-bit window table is one register per entry)
-#define LCV_DEF_POW_WAVE(fname, EXPARR, NBITS)                                            \
+#define LCV_DEF_POW_WAVE(fname, SCHED, NSCHED)                                            \
   LCV_FN void fname(fp& r, const fp& a_) {                                                \
     WaveTabs T;                                                                           \
     wv_tabs(T);                                                                           \
@@ -465,33 +465,23 @@ LCV_FN uint32_t* pow_lf_table() {
     tab[0] = a;                                                                           \
     const uint32_t a2 = wv_mul(a, a, T);                                                  \
     LCV_UNROLL for (int k = 1; k < 8; ++k) tab[k] = wv_mul(tab[k - 1], a2, T);            \
-    uint32_t acc = a;                                                                     \
-    bool started = false;                                                                 \
-    int i = (NBITS) - 1;                                                                  \
-    LCV_NOUNROLL while (i >= 0) {                                                         \
-      if (!((EXPARR[i >> 5] >> (i & 31)) & 1u)) {                                         \
-        acc = wv_mul(acc, acc, T);                                                        \
-        --i;                                                                              \
-        continue;                                                                         \
+    uint32_t e = SCHED[0], acc = tab[0];                                                  \
+    LCV_UNROLL for (int k = 1; k < 8; ++k) acc = (e >> 16) == (uint32_t)k ? tab[k] : acc; \
+    LCV_NOUNROLL for (int t = 1; t < (NSCHED); ++t) {                                     \
+      e = SCHED[t];                                                                       \
+      LCV_NOUNROLL for (uint32_t q = e & 0xFFFFu; q > 0; --q) acc = wv_mul(acc, acc, T);  \
+      const uint32_t idx = e >> 16;                                                       \
+      if (idx != 0xFFFFu) {                                                               \
+        uint32_t m = tab[0];                                                              \
+        LCV_UNROLL for (int k = 1; k < 8; ++k) m = idx == (uint32_t)k ? tab[k] : m;        \
+        acc = wv_mul(acc, m, T);                                                          \
       }                                                                                   \
-      int j = i - 3 < 0 ? 0 : i - 3;                                                      \
-      while (!((EXPARR[j >> 5] >> (j & 31)) & 1u)) ++j;                                   \
-      uint32_t w = 0;                                                                     \
-      for (int k = i; k >= j; --k) {                                                      \
-        w = (w << 1) | ((EXPARR[k >> 5] >> (k & 31)) & 1u);                               \
-        if (started) acc = wv_mul(acc, acc, T);                                           \
-      }                                                                                   \
-      uint32_t m = tab[0];                                                                \
-      LCV_UNROLL for (int k = 1; k < 8; ++k) m = (w >> 1) == (uint32_t)k ? tab[k] : m;     \
-      acc = started ? wv_mul(acc, m, T) : m;                                              \
-      started = true;                                                                     \
-      i = j - 1;                                                                          \
     }                                                                                     \
     wv_gather(L, acc);                                                                    \
     fp_lf_out(r, L);                                                                      \
   }
-LCV_DEF_POW_WAVE(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
-LCV_DEF_POW_WAVE(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)
+LCV_DEF_POW_WAVE(fp_pow_p1d4, LCV_SCHED_P_PLUS_1_DIV_4, LCV_SCHED_P_PLUS_1_DIV_4_N)  // sqrt candidate
+LCV_DEF_POW_WAVE(fp_pow_p3d4, LCV_SCHED_P_MINUS_3_DIV_4, LCV_SCHED_P_MINUS_3_DIV_4_N)
 #else
 LCV_DEF_POW_LF(fp_pow_p1d4, LCV_EXP_P_PLUS_1_DIV_4, LCV_EXP_P_PLUS_1_DIV_4_BITS)  // sqrt candidate
 LCV_DEF_POW_LF(fp_pow_p3d4, LCV_EXP_P_MINUS_3_DIV_4, LCV_EXP_P_MINUS_3_DIV_4_BITS)

@@ -14,6 +14,10 @@ for i in ${ROUNDS:-1 2}; do
     cp ${ABDIR:-abp}/liblcv_$v.so $LIB &&
     LCV_LAT_MODES=64 LCV_LAT_NS=1 LCV_LAT_REPS=20 timeout -k 10 200 python -u tools/latency_breakdown.py \
       > $OUT/lat_${v}_$i.json 2> $OUT/lat_${v}_$i.err || exit 1
+    if [ -n "${POW:-}" ]; then
+      timeout -k 10 120 python -u tools/pow_timing.py > $OUT/pow_${v}_$i.json 2> $OUT/pow_${v}_$i.err || exit 1
+      echo "$v $i pow $(cat $OUT/pow_${v}_$i.json)"
+    fi
     python -c "
 import json; d=json.load(open('$OUT/lat_${v}_$i.json'))['latency_engine_n1']
 s=d['stage_ms']; print('$v', $i, d['wall_ms_median'], {k: s[k] for k in ('nsc_htr','pre_checks','sig_decode','h2c_sswu','hash_to_g2','miller_loop','final_exp') if k in s})"
