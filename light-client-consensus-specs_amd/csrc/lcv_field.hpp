@@ -356,8 +356,8 @@ LCV_DEF_POW(fp_inv_fermat, LCV_EXP_P_MINUS_2, LCV_EXP_P_MINUS_2_BITS)    // a^(p
 // limb value < 2p squares to < 2p), so a product is its multiply-adds and quotient chain only.  In: a R ->
 // a 2^392 (one product with the raw constant 2^392 mod p); out: the chain's a^e 2^392 -> a^e R (one product
 // with 2^376) after packing and one subtraction.  Results equal the word-form walk's (both are fully reduced).
-// LCV_POW_LF 1 (the latency-mode twins, lcv_k_lat.hip): 4-bit window, table in LDS — a lone wave's SSWU maps
-// 1.55 -> 1.13 ms; at full batches the 28 KB LDS table per block crowds the co-resident final exponentiation
+// LCV_POW_LF 1 (the host simulation; the latency-mode twins until round 5 v6, now LCV_POW_LF 3 below): 4-bit
+// window, table in LDS — a lone wave's SSWU maps 1.55 -> 1.13 ms; at full batches the 28 KB LDS table per block crowds the co-resident final exponentiation
 // (LDS- and VGPR-bound at 12 waves per CU) and the serving loop measured 0.5-1 % slower.  LCV_POW_LF 2 (the
 // batch kernels): 3-bit window, four table entries in registers (the 4-bit register table spilled 624 B per
 // lane): serving loop +1.3 %, one batch at a time -3.7 % (profiles/r05_v5/pow_ab.txt).  0: the word form.

@@ -18,7 +18,8 @@ struct F_h2c_map { Work W; LCV_HD void operator()(uint32_t t) const { item_h2c_m
 struct F_sig { BatchDev B; Work W; LCV_HD void operator()(uint32_t i) const { item_sig(i, B, W); } };
 // latency-mode twins of the two one-lane-per-map/update kernels (lcv_k_lat.hip, compiled with LCV_FP_CALL=0:
 // the field products inlined, no call per product — ~14 % faster for a lone wave, ~2 % more chip cycles at
-// full batches, so batches keep the forms above)
+// full batches, so batches keep the forms above; and one item per wave, its square-root chains spread over the
+// wave, lcv_wave.hpp)
 struct F_h2c_map_lat { Work W; LCV_HD void operator()(uint32_t t) const { item_h2c_map(t, W); } };
 struct F_sig_lat { BatchDev B; Work W; LCV_HD void operator()(uint32_t i) const { item_sig(i, B, W); } };
 struct F_agg { BatchDev B; CommitteeDev C; Work W; LCV_HD void operator()(uint32_t i) const { item_agg(i, B, C, W); } };
