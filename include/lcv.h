@@ -149,11 +149,21 @@ int lcv_slot_allgather(lcv_ctx* ctx, int slot, uint64_t n, uint64_t per_rank, ui
 int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
 /* Latency mode for small batches (the reference's per-update usage: validate_light_client_update and
  * bls.FastAggregateVerify once per update, sync-protocol.md:512, :464): calls whose batch (or chunk) has
- * at most max_rows rows run the SOP programs (pairing, hash_to_G2 tail) on the fan engine — an op's K
- * products on K lanes, one update per block — instead of one op per lane.  Results are identical to the
- * batch engine's.  Default 64 (one update: 6.4 -> 5.0 ms on the MI355X); 0 = the batch
- * engine always.  Performance knob only. */
+ * at most max_rows rows run
+ *   - the SOP programs (hash_to_G2 tail, final exponentiation) on the fan engine — an op's K products on
+ *     K lanes, one update per block — instead of one op per lane,
+ *   - both Miller line walks and the accumulation as ONE fan-engine program (lines through LDS), and
+ *   - the SSWU maps and the signature decoding on their one-item-per-wave twins (each square-root
+ *     product spread over the 64 lanes of a wave).
+ * Results are identical to the batch engine's (bit for bit).  Default 64: one update 3.2 ms through
+ * lcv_validate_updates on the MI355X (6.1 ms on the batch engine); 0 = the batch engine
+ * always.  Performance knob only. */
 int lcv_set_latency_mode(lcv_ctx* ctx, uint64_t max_rows);
+/* test hook: which engines ran since the last reset (reset != 0 clears after reading).  out8[0] fan-engine
+ * SOP launches, [1] batch-engine SOP launches, [2] one-item-per-wave twin launches (SSWU / signature),
+ * [3] one-lane-per-item SSWU / signature launches, [4..7] items per wave of the last batch-engine launch of
+ * the line walk, Miller accumulation, final exponentiation, hash_to_G2 tail (0 = not launched) */
+int lcv_debug_engine_log(lcv_ctx* ctx, uint64_t* out8, int reset);
 /* kernel time of the last validate call: total and per stage (ms); names via lcv_stage_name
  * (stage times are recorded by the serial shape only: zero under a multi-stream pipeline) */
 int lcv_last_timings(lcv_ctx* ctx, float* ms_out, int max_stages, int* nstages);
@@ -239,8 +249,9 @@ int lcv_debug_set_chunk(lcv_ctx* ctx, uint64_t rows);
 /* test hook (host arithmetic only): allocates work-space slots 0 .. nslots-1 for `cap` rows and checks
  * (1) for slices of `slice` rows, that item j of each slice's work view is item base + j of the slot's
  * work space in every per-item field, element for element, as the kernels address them, and (2) that the
- * byte ranges of every field of every slot are pairwise disjoint.  LCV_EINVAL + lcv_last_error names the
- * first field that fails. */
+ * byte ranges of every field of every slot — the committee-pool fields (HTR roots and flags of a pool of 5
+ * distinct committees) included — are pairwise disjoint.  LCV_EINVAL + lcv_last_error names the first
+ * field that fails. */
 int lcv_debug_work_check(lcv_ctx* ctx, uint64_t cap, uint64_t slice, int nslots);
 /* test hook (device backend): hold work-space slot `slot`'s main stream with a kernel that waits for
  * lcv_debug_release_slots or max_seconds (<= 120), so that a collective behind it cannot complete */

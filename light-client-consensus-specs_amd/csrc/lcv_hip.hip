@@ -39,6 +39,7 @@ struct Backend {
   ncclComm_t comm = nullptr;  // RCCL communicator (lcv_comm_init), collectives on st[0]
   double* comm_scalar = nullptr;       // device scalar of lcv_comm_allreduce_max
   double* comm_host_scalar = nullptr;  // its pinned host staging (copies never block the bounded wait)
+  uint32_t* hold_flag = nullptr;       // lcv_debug_hold_slot's release word: pinned, mapped, this context's
 };
 
 static int be_init(lcv_ctx* ctx, int device);
@@ -55,7 +56,7 @@ static int be_join_from(lcv_ctx* ctx, int k);
 static int be_nstreams() { return BE_STREAMS; }
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
-template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
+template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n, uint32_t g);
 template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n);
 static int be_fork(lcv_ctx* ctx);
 static int be_join(lcv_ctx* ctx);
@@ -124,6 +125,8 @@ static void be_destroy(lcv_ctx* ctx) {
   for (int s = 0; s < LCV_SLOTS; ++s)
     for (int e = 0; e < EV_COUNT; ++e)
       if (ctx->be.ev[s][e]) (void)hipEventDestroy(ctx->be.ev[s][e]);
+  if (ctx->be.hold_flag) (void)hipHostFree(ctx->be.hold_flag);
+  ctx->be.hold_flag = nullptr;
 }
 
 static int be_alloc(lcv_ctx* ctx, void** p, size_t bytes) {
@@ -234,14 +237,10 @@ template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t 
   return LCV_OK;
 }
 
-template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n) {
+// g items per one-wave block (launch_sop, lcv_driver.inc)
+template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n, uint32_t g) {
   if (n == 0) return LCV_OK;
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  uint32_t g = 0;  // items per wave: the most that fit unless LCV_SOP_ITEMS_<PROGRAM> says fewer
-  if constexpr (std::is_same<F, F_sop_lines>::value) g = ctx->sop_items[0];
-  if constexpr (std::is_same<F, F_sop_acc>::value) g = ctx->sop_items[1];
-  if constexpr (std::is_same<F, F_sop_fexp>::value) g = ctx->sop_items[2];
-  if constexpr (std::is_same<F, F_sop_h2c>::value) g = ctx->sop_items[3];
   HIPCHK(ctx, lcv_hip_launch_sop<F>(f, n, cur_stream(ctx), g));
   return LCV_OK;
 }
@@ -416,15 +415,17 @@ __global__ __launch_bounds__(64) void k_hold(const volatile uint32_t* flag, uint
   const uint64_t t0 = wall_clock64();
   while (*flag == 0u && wall_clock64() - t0 < max_ticks) __builtin_amdgcn_s_sleep(127);
 }
-static uint32_t* g_hold_flag = nullptr;  // pinned, mapped host word
+// The release word is the context's own (allocated on its device on first use, freed by be_destroy), so
+// lcv_debug_release_slots(ctx) releases only this context's holds.
 extern "C" int lcv_debug_hold_slot(lcv_ctx* ctx, int slot, double max_seconds) {
   if (!ctx || slot < 0 || slot >= LCV_SLOTS || !(max_seconds > 0.0) || max_seconds > 120.0)
     return fail(ctx, LCV_EINVAL, "lcv_debug_hold_slot: slot 0..7, 0 < max_seconds <= 120");
   HIPCHK(ctx, hipSetDevice(ctx->be.device));
-  if (!g_hold_flag) HIPCHK(ctx, hipHostMalloc((void**)&g_hold_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  __atomic_store_n(g_hold_flag, 0u, __ATOMIC_SEQ_CST);
+  if (!ctx->be.hold_flag)
+    HIPCHK(ctx, hipHostMalloc((void**)&ctx->be.hold_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  __atomic_store_n(ctx->be.hold_flag, 0u, __ATOMIC_SEQ_CST);
   uint32_t* dflag = nullptr;
-  HIPCHK(ctx, hipHostGetDevicePointer((void**)&dflag, g_hold_flag, 0));
+  HIPCHK(ctx, hipHostGetDevicePointer((void**)&dflag, ctx->be.hold_flag, 0));
   int khz = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->be.device));
   const uint64_t ticks = (uint64_t)(max_seconds * 1e3 * (double)(khz > 0 ? khz : 100000));
@@ -434,7 +435,7 @@ extern "C" int lcv_debug_hold_slot(lcv_ctx* ctx, int slot, double max_seconds) {
 }
 extern "C" int lcv_debug_release_slots(lcv_ctx* ctx) {
   if (!ctx) return LCV_EINVAL;
-  if (g_hold_flag) __atomic_store_n(g_hold_flag, 1u, __ATOMIC_SEQ_CST);
+  if (ctx->be.hold_flag) __atomic_store_n(ctx->be.hold_flag, 1u, __ATOMIC_SEQ_CST);
   return LCV_OK;
 }
 

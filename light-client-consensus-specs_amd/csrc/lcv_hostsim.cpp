@@ -49,7 +49,7 @@ static int be_memset(lcv_ctx* ctx, void* p, int v, size_t bytes);
 static int be_sync(lcv_ctx* ctx);
 template <class F> static int be_launch(lcv_ctx* ctx, const F& f, uint32_t n);
 template <class F> static int be_launch_team(lcv_ctx* ctx, const F& f, uint32_t n);
-template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n);
+template <class F> static int be_launch_sop(lcv_ctx* ctx, const F& f, uint32_t n, uint32_t g = 0);
 // the latency engine's launches run the same per-item code (the device spreads products over lanes)
 // the fan engine (device latency mode) computes the batch engine's values: the simulation runs the latter
 template <class F> static int be_launch_sop_fan(lcv_ctx* ctx, const F& f, uint32_t n) { return be_launch_sop(ctx, f, n); }
@@ -120,7 +120,7 @@ template <class F> static int be_launch_team(lcv_ctx*, const F& f, uint32_t n) {
 static void be_use_stream(lcv_ctx* ctx, int k) { ctx->be.cur = (k > 0 && k < 4) ? k : 0; }
 // SOP team kernels: every lane of a round reads the item's LDS as it was when the round began (the
 // device's lockstep wave), so the rounds run lane by lane against a snapshot
-template <class F> static int be_launch_sop(lcv_ctx*, const F& f, uint32_t n) {
+template <class F> static int be_launch_sop(lcv_ctx*, const F& f, uint32_t n, uint32_t) {
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t i = 0; i < (int64_t)n; ++i) {
     std::vector<uint32_t> lds(F::LDS_WORDS, 0u), snap(F::LDS_WORDS, 0u), cl(F::SHARED_WORDS + 1, 0u);

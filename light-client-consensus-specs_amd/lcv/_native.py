@@ -75,6 +75,7 @@ SIGNATURES = {
     "lcv_last_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
     "lcv_set_pipeline": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "lcv_set_latency_mode": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "lcv_debug_engine_log": (C.c_int, [C.c_void_p, u64p, C.c_int]),
     "lcv_set_config": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "lcv_stage_name": (C.c_char_p, [C.c_int]),
     "lcv_comm_unique_id": (C.c_int, [u8p]),

@@ -149,12 +149,25 @@ class Comm:
 
         The grace period is at least the communicator timeout: survivors detect the failure when their
         own collective times out, which starts when each enters its wait, so a slower survivor announces
-        up to one timeout after the first."""
+        up to one timeout after the first.  It is counted from the FIRST announcement (the earliest alive
+        marker), not from this rank's own, so every survivor decides at the same moment.  Recovery latency:
+        a dead rank never announces itself, so a recovery takes one communicator timeout to detect the
+        failure (the bounded collective wait) plus up to max(grace, timeout) here — with the default 60 s
+        timeout about two minutes; lower it with Comm(timeout=...) / set_timeout where peers are fast."""
         grace = max(float(grace), getattr(self, "timeout", 0.0))
         me = self.ranks[self.rank]
         open(self._fail_path(f"alive.{me}"), "w").close()
-        t0 = time.monotonic()
-        while time.monotonic() - t0 < grace:
+
+        def first_announcement() -> float:
+            ts = []
+            for r in self.ranks:
+                try:
+                    ts.append(os.stat(self._fail_path(f"alive.{r}")).st_mtime)
+                except FileNotFoundError:
+                    pass
+            return min(ts) if ts else time.time()
+
+        while time.time() - first_announcement() < grace:
             if all(os.path.exists(self._fail_path(f"alive.{r}")) for r in self.ranks):
                 break
             if os.path.exists(self._fail_path("decision")):

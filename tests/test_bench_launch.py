@@ -28,7 +28,7 @@ def _run(extra_env, args, timeout=600):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_gpus_n_spawns_n_ranks(world):
     p = _run({"OMP_NUM_THREADS": "1" if world > 2 else "2"}, ["--gpus", str(world)] + ARGS)
     assert p.returncode == 0, p.stderr[-2000:]

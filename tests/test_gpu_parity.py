@@ -57,7 +57,7 @@ def test_sign_kat(gpu_verifier):
     assert not gpu_verifier.fast_aggregate_verify([pk], b"\x01" * 32, sig)
 
 
-def test_pairing_value(gpu_verifier):
+def test_pairing_value(engine_verifier):
     rng = np.random.default_rng(3)
     ps, qs, exp = [], [], []
     for _ in range(2):
@@ -67,19 +67,19 @@ def test_pairing_value(gpu_verifier):
         qs.append(b"".join(c.to_bytes(48, "big") for c in (Q[0][0], Q[0][1], Q[1][0], Q[1][1])))
         e = B.pairing(P, Q)
         exp.append(B.f12_mul(B.f12_mul(e, e), e))  # device returns e^3
-    out = gpu_verifier.debug_pairing(np.frombuffer(b"".join(ps), np.uint8), np.frombuffer(b"".join(qs), np.uint8))
+    out = engine_verifier.debug_pairing(np.frombuffer(b"".join(ps), np.uint8), np.frombuffer(b"".join(qs), np.uint8))
     for i in range(2):
         g = _ints(out[i], 12)
         coeffs = [(g[2 * k], g[2 * k + 1]) for k in range(6)]
         assert B.f12_from_coeffs(coeffs) == exp[i]
 
 
-def test_validate_adversarial_vs_oracle(gpu_verifier):
+def test_validate_adversarial_vs_oracle(engine_verifier):
     from lcv import synth
     kinds = np.array([0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 0])
-    sb = synth.generate(gpu_verifier, len(kinds), seed=7, participation="random", kinds=kinds)
-    gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
-    ok, reason = gpu_verifier.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    sb = synth.generate(engine_verifier, len(kinds), seed=7, participation="random", kinds=kinds)
+    engine_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    ok, reason = engine_verifier.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
     store = H.store_from(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     exp = [H.O.validate_light_client_update(store, H.update_from(sb.updates, i), sb.current_slot,
                                             sb.genesis_validators_root) for i in range(len(kinds))]
@@ -111,18 +111,18 @@ def test_validate_large_batch_properties(gpu_verifier):
         gpu_verifier.set_pipeline(1, 1)
 
 
-def test_store_sequence_on_gpu(gpu_verifier):
+def test_store_sequence_on_gpu(engine_verifier):
     """lcv.store over liblcv.so reproduces the reference's exec'd process_light_client_update
     sequence (tests/golden/store_sequence.npz) step by step and in the batched form."""
     import store_cases
-    store_cases.run(gpu_verifier)
+    store_cases.run(engine_verifier)
 
 
-def test_validate_non_subgroup_signature(gpu_verifier):
+def test_validate_non_subgroup_signature(engine_verifier):
     """Signatures that decode to curve points outside G2 (or to the identity) fail at :464 on the
     validate path, where the G2 subgroup check is fused into the signature pairing's line walk."""
     from lcv import synth
-    sb = synth.generate(gpu_verifier, 6, seed=9)
+    sb = synth.generate(engine_verifier, 6, seed=9)
     sigs = sb.updates.sync_signature
     x, bad = 1, []
     while len(bad) < 3:
@@ -134,8 +134,8 @@ def test_validate_non_subgroup_signature(gpu_verifier):
     for row, s in zip((1, 3, 4), bad):
         sigs[row] = np.frombuffer(s, np.uint8)
     sigs[5] = np.frombuffer(bytes([0xC0]) + bytes(95), np.uint8)  # identity signature
-    gpu_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
-    ok, reason = gpu_verifier.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
+    engine_verifier.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
+    ok, reason = engine_verifier.validate(sb.updates, sb.current_slot, sb.genesis_validators_root)
     store = H.store_from(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
     exp = [H.O.validate_light_client_update(store, H.update_from(sb.updates, i), sb.current_slot,
                                             sb.genesis_validators_root) for i in range(6)]

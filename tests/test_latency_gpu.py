@@ -88,39 +88,56 @@ def test_latency_engine_fast_aggregate_verify(gpu_verifier):
     assert a == b == (True, False)
 
 
-@pytest.mark.parametrize("items", [1, 5, 6])
-def test_h2c_items_per_wave(gpu_verifier, items, monkeypatch):
-    """hash_to_G2's tail with fewer items per wave (LCV_SOP_ITEMS_H2C, read at lcv_init): a ragged batch
-    (37 messages: partial last wave) gives the default launch's points bit for bit, and the oracle's."""
+def _knob_verifier(monkeypatch, env):
+    """A fresh context (LCV_SOP_ITEMS_* are read at lcv_init) in latency mode 0, so that every SOP launch
+    takes the batch engine — the only engine that reads the knob."""
     import os
     from lcv.device import Verifier
+    for k, val in env.items():
+        monkeypatch.setenv(k, str(val))
+    v = H.hostsim_verifier() if os.environ.get("LCV_TEST_HOSTSIM") == "1" else Verifier(0)
+    v.set_latency_mode(0)
+    v.engine_log(reset=True)
+    return v
+
+
+@pytest.mark.parametrize("items", [1, 5, 6])
+def test_h2c_items_per_wave(engine_verifier, items, monkeypatch):
+    """hash_to_G2's tail on the batch engine with fewer items per wave (LCV_SOP_ITEMS_H2C, read at lcv_init): a
+    ragged batch (37 messages: partial last wave) gives both engines' default launches' points bit for bit,
+    and the oracle's; the engine log proves the batch engine ran h2c at `items` per wave."""
     rng = random.Random(60 + items)
     msgs = np.frombuffer(bytes(rng.randrange(256) for _ in range(32 * 37)), np.uint8)
-    h_ref, i_ref = gpu_verifier.debug_hash_to_g2(msgs)
-    monkeypatch.setenv("LCV_SOP_ITEMS_H2C", str(items))
-    v = H.hostsim_verifier() if os.environ.get("LCV_TEST_HOSTSIM") == "1" else Verifier(0)
+    h_ref, i_ref = engine_verifier.debug_hash_to_g2(msgs)  # default launch of the parametrized engine
+    v = _knob_verifier(monkeypatch, {"LCV_SOP_ITEMS_H2C": items})
     h, inf = v.debug_hash_to_g2(msgs)
+    log = v.engine_log()
+    assert log["fan"] == 0 and log["batch"] > 0 and log["items"]["h2c"] == items, log
     assert np.array_equal(h, h_ref) and np.array_equal(inf, i_ref)
     for i in (0, 36):
         e = B.hash_to_g2(msgs[32 * i:32 * i + 32].tobytes())
         got = [int.from_bytes(h[i][48 * k:48 * k + 48].tobytes(), "big") for k in range(4)]
         assert got == [e[0][0], e[0][1], e[1][0], e[1][1]]
+    v.close()
 
 
 @pytest.mark.parametrize("items", [3, 4])
-def test_pairing_items_per_wave(gpu_verifier, items, monkeypatch):
-    """The pairing's SOP kernels (line walk, Miller accumulation, final exponentiation) with fewer items per
-    wave (LCV_SOP_ITEMS_LINES / _ACC / _FEXP): pairing values of a ragged batch equal the default launch's."""
-    import os
-    from lcv.device import Verifier
+def test_pairing_items_per_wave(engine_verifier, items, monkeypatch):
+    """The pairing's SOP kernels on the batch engine (line walk, Miller accumulation, final exponentiation) with
+    fewer items per wave (LCV_SOP_ITEMS_LINES / _ACC / _FEXP): pairing values of a ragged batch (7 items) equal
+    both engines' default launches'; the engine log proves each program ran at `items` per wave."""
     rng = random.Random(70 + items)
     ps = [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(7)]
     qs = [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(7)]
     p96 = np.frombuffer(b"".join(x.to_bytes(48, "big") + y.to_bytes(48, "big") for x, y in ps), np.uint8)
     q192 = np.frombuffer(b"".join(q[0][0].to_bytes(48, "big") + q[0][1].to_bytes(48, "big") + q[1][0].to_bytes(48, "big")
                                   + q[1][1].to_bytes(48, "big") for q in qs), np.uint8)
-    ref = gpu_verifier.debug_pairing(p96, q192)
-    for name in ("LINES", "ACC", "FEXP"):
-        monkeypatch.setenv(f"LCV_SOP_ITEMS_{name}", str(items))
-    v = H.hostsim_verifier() if os.environ.get("LCV_TEST_HOSTSIM") == "1" else Verifier(0)
+    ref = engine_verifier.debug_pairing(p96, q192)
+    v = _knob_verifier(monkeypatch, {f"LCV_SOP_ITEMS_{name}": items for name in ("LINES", "ACC", "FEXP")})
     assert np.array_equal(v.debug_pairing(p96, q192), ref)
+    log = v.engine_log()
+    assert log["fan"] == 0 and log["items"] == {"lines": items, "miller_acc": items, "fexp": items, "h2c": 0}, log
+    e = B.pairing(ps[6], qs[6])
+    e3 = B.f12_coeffs(B.f12_mul(B.f12_mul(e, e), e))
+    assert [int.from_bytes(ref[6][48 * k:48 * k + 48].tobytes(), "big") for k in range(12)] == [c for g in e3 for c in g]
+    v.close()

@@ -28,7 +28,8 @@ def _worker(rank, world, port, q):
     try:
         from lcv import multi, synth
         v = H.hostsim_verifier()
-        kinds = np.array([0, 2, 4, 1, 5, 0, 6])
+        # 7 rows over 2 ranks; 8 k + 5 = 21 rows over 8 ranks (north_star's width): uneven shards, padded slices
+        kinds = np.array([0, 2, 4, 1, 5, 0, 6] * (1 if world <= 2 else 3))
         sb = synth.generate(v, len(kinds), seed=31, kinds=kinds)  # identical on every rank (seeded)
         v.set_store(sb.store_finalized_slot, sb.current.ssz, sb.next.ssz)
         comm = multi.Comm(v, world, rank, key=f"test_{port}")
@@ -67,22 +68,27 @@ def test_shard_bounds():
             assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
 
 
-@pytest.mark.timeout(600)
-def test_two_rank_gloo():
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world", [2, 8])
+def test_two_rank_gloo(world):
+    """world 2, and world 8 (the north_star's 8-GPU split) with 8 k + 5 rows: every rank's gathered verdicts
+    (validate_sharded and the per-slot all-gathers) equal the construction, the gloo all-gather of the same
+    shards and the single-rank result."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=500) for _ in range(2)]
+    res = [q.get(timeout=800) for _ in range(world)]
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == list(range(world))
     for rank, full, gloo, exp, t, slots in res:
         assert full == exp == gloo == slots[0] == slots[1]
-        assert t == 2.0
+        assert t == float(world)
 
 
 def _inject_failure(multi, dead, mode):

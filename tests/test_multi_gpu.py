@@ -71,35 +71,34 @@ def test_rccl_failure_entries_one_rank(gpu_verifier):
 
 
 def test_collective_behind_held_stream_fails_within_timeout(gpu_verifier):
-    """a collective that cannot complete must fail the call within the communicator
-    timeout — the bounded wait comes before any copy into the caller's pageable memory, which would block
-    the host until the stream reached it.  The slot's main stream is held by a spinning one-wave kernel
-    (lcv_debug_hold_slot: it exits when released or after 20 s), so the all-gather and the all-reduce
-    behind it cannot complete: each call must raise CommFailed in about the 2 s timeout, not return after
-    the hold."""
+    """ADVICE r04 (medium), VERDICT r05 item 5: a collective that cannot complete must fail the call within the
+    communicator timeout, from the FIRST call on a fresh communicator — the communication buffer is sized at
+    lcv_comm_init and grows without a free (a free waits for every stream without bound), and the bounded wait
+    comes before any copy into the caller's pageable memory.  The slot's main stream is held by a spinning
+    one-wave kernel (lcv_debug_hold_slot: it exits when released or after 20 s), so the collective behind it
+    cannot complete: each call — a per-slot all-gather within the pre-sized buffer, one whose per_rank
+    outgrows it, and the all-reduce — must raise CommFailed in about the 2 s timeout, not return after the
+    hold."""
     if os.environ.get("LCV_TEST_HOSTSIM") == "1":
         pytest.skip("device streams: product library only")
     import time
     from lcv import multi
     v = gpu_verifier
-    for what in ("slot_allgather", "allreduce_max"):
-        comm = multi.Comm(v, 1, 0, key=f"gputest_hold_{what}_{os.getpid()}", timeout=2.0)
+    for what, per_rank in (("slot_allgather", 64), ("slot_allgather", 3 * 65536 + 64), ("allreduce_max", 0)):
+        comm = multi.Comm(v, 1, 0, key=f"gputest_hold_{what}_{per_rank}_{os.getpid()}", timeout=2.0)
         try:
-            # the same call once unheld first: it sizes the communication buffer (growing it later would
-            # free the old one, which waits for every stream, the held one included)
-            assert comm.slot_allgather(0, 0, 64).shape == (64,) and comm.allreduce_max(1.0) == 1.0
             assert v.lib.lcv_debug_hold_slot(v.ctx, 0, 20.0) == 0
             t0 = time.monotonic()
             try:
                 with pytest.raises(multi.CommFailed):
                     if what == "slot_allgather":
-                        comm.slot_allgather(0, 0, 64)
+                        comm.slot_allgather(0, 0, per_rank)
                     else:
                         comm.allreduce_max(1.0)
                 dt = time.monotonic() - t0
             finally:
                 v.lib.lcv_debug_release_slots(v.ctx)
-            assert dt < 10.0, dt
+            assert dt < 10.0, (what, per_rank, dt)
             comm.abort()
         finally:
             v.lib.lcv_debug_release_slots(v.ctx)

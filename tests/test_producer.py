@@ -62,6 +62,6 @@ def test_produced_updates_validate_hostsim(sim_verifier):
 
 
 @pytest.mark.gpu
-def test_produced_updates_validate_gpu(gpu_verifier):
+def test_produced_updates_validate_gpu(engine_verifier):
     z, cases = PC.load()
-    assert _validate(gpu_verifier, z, cases) == [c["reason"] for c in cases]
+    assert _validate(engine_verifier, z, cases) == [c["reason"] for c in cases]

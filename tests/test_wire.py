@@ -229,20 +229,21 @@ def validate_decoded(v, batch, rows, g):
 
 
 @pytest.mark.gpu
-def test_bootstrap_checks_gpu(gpu_verifier):
-    got, exp, _, _ = run_bootstrap_cases(gpu_verifier)
+@pytest.mark.no_sop
+def test_bootstrap_checks_gpu(engine_verifier):
+    got, exp, _, _ = run_bootstrap_cases(engine_verifier)
     assert got.tolist() == exp.tolist()
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", [0, 1, 2])
-def test_decode_then_validate_gpu(gpu_verifier, kind):
+def test_decode_then_validate_gpu(engine_verifier, kind):
     """SSZ bytes (serialised by the reference's containers) -> native decode -> device validation."""
     w, g = load_wire(), load_updates()
     sel = np.flatnonzero(w["kind"] == kind)
     rows = w["row"][sel]
-    batch = wire.decode_updates(messages(w, sel), kind=["update", "finality", "optimistic"][kind], lib=gpu_verifier.lib)
-    got, exp = validate_decoded(gpu_verifier, batch, rows, g)
+    batch = wire.decode_updates(messages(w, sel), kind=["update", "finality", "optimistic"][kind], lib=engine_verifier.lib)
+    got, exp = validate_decoded(engine_verifier, batch, rows, g)
     assert got.tolist() == exp.tolist()
     if kind == 0:
         assert got.tolist() == g["expected_reason"][rows].tolist()
