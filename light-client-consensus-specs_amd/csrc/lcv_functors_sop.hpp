@@ -31,10 +31,14 @@ enum { SOP_PITCH_PAD = LCV_SOP_B128 ? 4 : 1 };
 // 32-bit accesses (a bank model: 1.3-1.4x the conflict-free LDS cycles instead of 2.7-3.4x); since r03
 // v13 the pitch is 4 mod 8 words and values move as 16-byte accesses, three instead of six LDS
 // instructions per value: 1.448 -> 1.472 M updates/s in a same-box A/B (profiles/r03_v13)
+// the SOP kernels' VGPR budget in waves per SIMD (3 = 168 VGPRs, no spills; an experiment knob)
+#ifndef LCV_SOP_WAVES
+#define LCV_SOP_WAVES 3
+#endif
 struct F_sop_lines {
   Work W; SopView P;
   uint32_t mode;  // 0: items t = 2i + k (both pairings); 1: t = i, k = 1 (signature); 2: t = i, k = 0 (message)
-  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = LCV_SOP_WAVES;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_LINES_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;    // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_LINES_TEAM, LDS_WORDS = LCV_SOP_LINES_SLOTS * 12 + SOP_PITCH_PAD,
@@ -107,7 +111,7 @@ struct F_sop_lines {
 
 struct F_sop_acc {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = LCV_SOP_WAVES;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_MILLER_ACC_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;         // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_MILLER_ACC_TEAM, LDS_WORDS = LCV_SOP_MILLER_ACC_SLOTS * 12 + SOP_PITCH_PAD,
@@ -220,7 +224,7 @@ struct F_sop_miller {
 
 struct F_sop_fexp {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = LCV_SOP_WAVES;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_FEXP_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;   // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_FEXP_TEAM, LDS_WORDS = LCV_SOP_FEXP_SLOTS * 12 + SOP_PITCH_PAD,
@@ -266,7 +270,7 @@ struct F_sop_fexp {
 // formulas), affine H(m) -> W.qh and its identity flag -> W.qh_inf
 struct F_sop_h2c {
   Work W; SopView P;
-  static constexpr uint32_t WAVES = 3;  // waves per SIMD the kernel's VGPR budget targets
+  static constexpr uint32_t WAVES = LCV_SOP_WAVES;  // waves per SIMD the kernel's VGPR budget targets
   static constexpr uint32_t MAXK = LCV_SOP_H2C_MAXK;  // the fan engine's lanes per op
   static constexpr uint32_t FAN_PARTS = LCV_FAN_PARTS;  // the fan engine's lanes per product
   static constexpr uint32_t TEAM = LCV_SOP_H2C_TEAM, LDS_WORDS = LCV_SOP_H2C_SLOTS * 12 + SOP_PITCH_PAD,

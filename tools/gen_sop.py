@@ -673,28 +673,42 @@ def fp12_mul_line_ops(f, line, out):
     return ops
 
 
-def cyclo_sqr_ops(g, out):
+def cyclo_sqr_ops(g, out, cin=1, cout=1):
     """Granger-Scott cyclotomic squaring, one round: z = [3A0 - 2g0, 3 xi C1 + 2g1, 3B0 - 2g2,
     3A1 + 2g3, 3C0 - 2g4, 3B1 + 2g5] with (A0, A1) = (g0^2 + xi g3^2, 2 g0 g3), (B0, B1) from (g1, g4),
-    (C0, C1) from (g2, g5).  12 ops, <= 3 products + one add-in each."""
+    (C0, C1) from (g2, g5).  12 ops, <= 3 products + one add-in each.
+    Scaled values (fexp_program's scaled chain): the slots of g hold cin * g and out receives cout * z, so
+    the products take m = 3 cout / cin^2 (6 cout / cin^2 for the 2 x y terms) and the add-ins 2 cout / cin:
+    (1, 1) m = 3 / 6 (every product of the round m-scaled on the device), (3, 3) m = 1 / 2 (the 2 folds
+    into a doubled operand: no m-scaling), (1, 3) m = 9 / 18, add-ins 6."""
+    from fractions import Fraction as Fr
+    ms, mp_, ma = Fr(3 * cout, cin * cin), Fr(6 * cout, cin * cin), Fr(2 * cout, cin)
+    assert ms.denominator == mp_.denominator == ma.denominator == 1, (cin, cout)
+    ms, mp_, ma = int(ms), int(mp_), int(ma)
     ops = []
     pairs = {0: (0, 3), 2: (1, 4), 4: (2, 5)}   # output index -> (x0, x1) of its Fp4 square, "0" part
     for k in range(6):
         for comp in range(2):
-            add_c = 2 if k % 2 else -2
+            add_c = ma if k % 2 else -ma
             gk = g[k][comp]
             adds = [(gk.slot, add_c if not gk.neg else -add_c)]
             if k in (0, 2, 4):   # 3 (x0^2 + xi x1^2) - 2 g_k  with (x0, x1) = (g0, g3) | (g1, g4) | (g2, g5)
                 x0, x1 = pairs[k]
-                prods = fp2_sqr(g[x0], comp, False, 3) + fp2_sqr(g[x1], comp, True, 3)
+                prods = fp2_sqr(g[x0], comp, False, ms) + fp2_sqr(g[x1], comp, True, ms)
             elif k == 3:         # 3 * 2 g0 g3 + 2 g3
-                prods = fp2_prod(g[0], g[3], comp, False, 6)
+                prods = fp2_prod(g[0], g[3], comp, False, mp_)
             elif k == 5:         # 3 * 2 g1 g4 + 2 g5
-                prods = fp2_prod(g[1], g[4], comp, False, 6)
+                prods = fp2_prod(g[1], g[4], comp, False, mp_)
             else:                # k == 1: 3 xi (2 g2 g5) + 2 g1
-                prods = fp2_prod(g[2], g[5], comp, True, 6)
+                prods = fp2_prod(g[2], g[5], comp, True, mp_)
             ops.append(Op(dst_of(out[k][comp]), prods, adds))
     return ops
+
+
+def scale_ops(p, src, dst, c):
+    """dst = c * src for a constant c (12 ops of one product each; views may carry negations)."""
+    cc = T(p.const(c))
+    return [Op(dst_of(d), [([s], [cc], 1)]) for s, d in zip(flat12(src), flat12(dst))]
 
 
 def copy_ops(src, dst):
@@ -968,6 +982,7 @@ def frob_ops(p, a, k, out):
 def fexp_program_r03(team=12):
     """f^((p^12 - 1)/r) * 3 (result e^3): easy part
     (p^6 - 1)(p^2 + 1) with a team-parallel Fp12 inversion, hard part (x-1)^2 (x+p)(x^2+p^2-1) + 3."""
+    scaled = FEXP_SCALED if scaled is None else scaled
     p = Program("fexp", team)
     f = fp12_slots(p, "f")
     c0 = [f[0], f[2], f[4]]   # Fp6 halves in the v basis
@@ -1075,7 +1090,10 @@ def fexp_program_r03(team=12):
     return p
 
 
-def fexp_program(team=12):
+FEXP_SCALED = os.environ.get("LCV_SOP_FEXP_SCALED", "1") == "1"   # A/B: 0 = round 5's m-scaled chains
+
+
+def fexp_program(team=12, scaled=None):
     """f^((p^12 - 1)/r) * 3 (result e^3), three live Fp12 values in the hard part (r04): easy part
     (p^6 - 1)(p^2 + 1) with a team-parallel Fp12 inversion whose temporaries are released as soon as
     they die, then with m = f^((p^6 - 1)(p^2 + 1)), x < 0, e() = exponentiation by |x| (e(a) = a^-x):
@@ -1088,6 +1106,7 @@ def fexp_program(team=12):
     Every product reads negated values only on its x side (fp2_prod negx, the exponentiation's running
     value), so the chains' bases need no shadow slots: LDS per item 79 -> fewer slots, a third wave per
     SIMD."""
+    scaled = FEXP_SCALED if scaled is None else scaled
     p = Program("fexp", team)
     f = fp12_slots(p, "f")
     c0 = [f[0], f[2], f[4]]   # Fp6 halves in the v basis
@@ -1160,14 +1179,30 @@ def fexp_program(team=12):
     F2 = fp12_slots(p)
     F3 = fp12_slots(p)
 
+    # Scaled chains (scaled = FEXP_SCALED, r06): each exponentiation's running value is stored as 3 z, so its
+    # 62 squarings after the first are Granger-Scott with m = 1 (products) and 2 (folded into a doubled
+    # operand): no m-scaled product rounds (the device's m X costs 12 multiply-adds and as many moves per
+    # product).  The first squaring reads the unscaled base (m = 9), the multiplications 3 z * a keep the
+    # scale (the base a unscaled), and each chain result that becomes a base or the output is brought back
+    # by a product with the constant 1/3 (a one-product round): 5 such rounds against 310 unscaled squarings.
+    inv3 = pow(3, -1, P)
+
     def exp_x(a, out):
-        """out = a^|x| (a cyclotomic; `out` must differ from a's slots); negated reads on out only."""
+        """out = a^|x| (a cyclotomic; `out` must differ from a's slots); negated reads on out only.
+        scaled: out holds 3 a^|x|."""
         firstsq = True
         for bit in bin(X_ABS)[3:]:
-            p.round(cyclo_sqr_ops(a if firstsq else out, out))
+            if scaled:
+                p.round(cyclo_sqr_ops(a if firstsq else out, out, 1 if firstsq else 3, 3))
+            else:
+                p.round(cyclo_sqr_ops(a if firstsq else out, out))
             firstsq = False
             if bit == "1":
                 p.round(fp12_mul_ops(out, a, out, negx=True))
+
+    def unscale(v):
+        if scaled:
+            p.round(scale_ops(p, v, v, inv3))
 
     # F2 = m^3 (negated reads on m, whose shadows the squarings need anyway)
     p.round(cyclo_sqr_ops(F1, F2))
@@ -1175,13 +1210,16 @@ def fexp_program(team=12):
     # A = conj(e(m) m) into F1
     exp_x(F1, F3)
     p.round(fp12_mul_ops(F3, F1, F1, negx=True, conj_out=True))
+    unscale(F1)
     # A2 = conj(e(A) A) into F1
     exp_x(F1, F3)
     p.round(fp12_mul_ops(F3, F1, F1, negx=True, conj_out=True))
+    unscale(F1)
     # Bv = conj(e(A2)) frob1(A2) into F1
     exp_x(F1, F3)
     p.round(frob_ops(p, F1, 1, F1))
     p.round(fp12_mul_ops(conj12(F3), F1, F1, negx=True))
+    unscale(F1)
     # F3 = frob2(Bv) conj(Bv) (conj's signs on F3's reads); F2 = m^3 F3; Bv re-stored (a product-free
     # copy round: its negated shadows are written there, just before the chain's first squaring reads
     # them, instead of living from Bv's product through these rounds); F3 = e(Bv); F1 = e(F3); r = F1 F2
@@ -1190,8 +1228,10 @@ def fexp_program(team=12):
     p.round(fp12_mul_ops(F3, F2, F2, negx=True))
     p.round(copy_ops(flat12(F1), flat12(F1)))
     exp_x(F1, F3)
+    unscale(F3)
     exp_x(F3, F1)
     p.round(fp12_mul_ops(F1, F2, F2, negx=True))
+    unscale(F2)
     for i in range(6):
         for c in range(2):
             p.named[f"r{i}_{c}"] = F2[i][c].slot
