@@ -204,6 +204,7 @@ LCV_FN void fp_sqr_c28(uint32_t r[13], const uint32_t a[12]) {
 
 // limb-form Montgomery square / product with R = 2^392 (values < 2p stay < 2p: (T + M p) / R < 4p^2 / R + p)
 LCV_FN void fp_sqr_lf(uint32_t r[14], const uint32_t a[14]) {
+  LCV_COUNT(0);  // op counter (host simulation, -DLCV_OPCOUNT): one Fp multiplication
   int32_t d[7];
   LCV_UNROLL for (int i = 0; i < 7; ++i) d[i] = (int32_t)(a[i] - a[i + 7]);
   uint64_t p0[13], p2[13], col[28];
@@ -216,6 +217,7 @@ LCV_FN void fp_sqr_lf(uint32_t r[14], const uint32_t a[14]) {
   sop_redc28_392(r, col);
 }
 LCV_FN void fp_mul_lf(uint32_t r[14], const uint32_t a[14], const uint32_t b[14]) {
+  LCV_COUNT(0);
   uint32_t x[15];
   LCV_UNROLL for (int i = 0; i < 14; ++i) x[i] = a[i];
   x[14] = 0;
