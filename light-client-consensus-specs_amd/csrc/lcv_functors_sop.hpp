@@ -412,7 +412,7 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
   };
   Rec nx = fetch(0);
 #if LCV_FAN_X_TIMING
-  uint64_t tq[5] = {0, 0, 0, 0, 0}, tp = clock64();
+  uint64_t tq[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tp = clock64();
 #define LCV_FAN_T(i) do { const uint64_t tn = clock64(); tq[i] += tn - tp; tp = tn; } while (0)
 #else
 #define LCV_FAN_T(i) ((void)0)
@@ -449,11 +449,27 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
         uint64_t col[28];
         LCV_UNROLL for (int c = 0; c < 28; ++c) col[c] = acc[c];
         LCV_UNROLL for (int c = 0; c < 28; ++c) acc[c] = 0;
+#if LCV_FAN_X_TIMING > 1  // sub-phases of the tail (the sums wait for their reads: the clock reads data)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        LCV_FAN_T(5);
+#endif
         lcv::sop_redc28(res, col);
+#if LCV_FAN_X_TIMING > 1
+        asm volatile("" :: "v"(res[12]));
+        LCV_FAN_T(6);
+#endif
       }
       lcv::fp v;
       lcv::sop_tail_value(v, h0, cur.w, cur.pre, my, lds, ns, res, qp);
+#if LCV_FAN_X_TIMING > 1
+      asm volatile("" :: "v"(v.v[11]));
+      LCV_FAN_T(7);
+#endif
       lcv::sop_tail_store(h0, cur.pre, my, io_in, io_out, v);
+#if LCV_FAN_X_TIMING > 1
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      LCV_FAN_T(8);
+#endif
     }
     LCV_FAN_T(3);
     __syncthreads();
@@ -461,8 +477,9 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
   }
 #if LCV_FAN_X_TIMING
   if (item == 0 && (L == 0 || L == NT - 64))
-    printf("fan T=%u KM=%u S=%u R=%u wave=%u: fetch %lu products %lu barrier1 %lu tail %lu barrier2 %lu\n", T, KM, S,
-           R, L / 64, tq[0], tq[1], tq[2], tq[3], tq[4]);
+    printf("fan T=%u KM=%u S=%u R=%u wave=%u: fetch %lu products %lu barrier1 %lu tail %lu barrier2 %lu | tail: "
+           "columns %lu redc %lu value %lu store %lu\n", T, KM, S, R, L / 64, tq[0], tq[1], tq[2], tq[3], tq[4], tq[5],
+           tq[6], tq[7], tq[8]);
 #endif
 #undef LCV_FAN_T
   if (L < T && item < n) f.epilogue(item, L, my);
