@@ -11,6 +11,7 @@
 #include "lcv_sop_programs.inc"
 #if defined(LCV_KERNEL_UNIT)
 #include "lcv_sop_fan.hpp"
+#include "lcv_sop_row.hpp"
 #endif
 // the fan engine's lanes per product (lcv_sop_fan.hpp; also known to lcv_launch.hpp): 3 = Karatsuba parts split
 #ifndef LCV_FAN_SPLIT
@@ -368,9 +369,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
 #ifndef LCV_FAN_X_TIMING
 #define LCV_FAN_X_TIMING 0
 #endif
+// LCV_FAN_ROW (lcv_launch.hpp, the default) for the programs of at most LCV_FAN_ROW_MAX_TEAM ops a round
+// (lcv_fan_rows<F>: the final exponentiation and hash_to_G2's tail): op o's tail runs on the 16-lane row of lanes
+// 16 o .. 16 o + 15 (lcv_sop_row.hpp: the reduction as two column passes, one column pair per lane; the add-ins,
+// the quotient step and the store with a limb or word per lane), instead of on one lane of the first wave.  The
+// tails then sit in several waves, so a row reads its add-in terms at the top of the round, before any tail of
+// the round stores (ops update slots in place).  Inversion, side-load and emit rounds gather the value on the
+// row's lane 0, which runs the inversion flag and sop_tail_store as the one-lane tail does.
 template <class F>
-__global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64) void k_sop_fan(F f, uint32_t n) {
-  constexpr uint32_t T = F::TEAM, KM = F::MAXK, S = F::FAN_PARTS, NT = ((T * KM * S + 63) / 64) * 64;
+__global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t n) {
+  constexpr uint32_t T = F::TEAM, KM = F::MAXK, S = F::FAN_PARTS, NT = lcv_fan_threads<F>();
+  constexpr bool ROWS = lcv_fan_rows<F>();
   constexpr uint32_t ITEM_WORDS = (F::LDS_WORDS + 1u) & ~1u;  // 8-byte aligned scratch after the slots
   static_assert(T <= 64, "every op's tail lane in the first wave");
   static_assert(S == 1 || S == 3, "one lane per product, or one per Karatsuba part");
@@ -390,16 +399,37 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
   uint32_t* io_out = item < n ? f.io_out(item) : nullptr;
   const uint32_t R = f.P.rounds, ns = f.P.nslots;
   const lcv::SopBase base{my, lds, (int32_t)((const char*)lds - (const char*)my)};
-  // round r + 1's header and this lane's record words (its product's operand pair and scale; the tail
-  // lane's dst / io words) are loaded at the top of round r, so their latency overlaps round r's work
-  struct Rec { uint32_t h0, h3, x, y, m; lcv::SopPre pre; const uint32_t* w; };
-  auto fetch = [&](uint32_t r) {
+  // the tail's op and lane: op L >> 4 on its row's lane 0 (ROWS), else op L on lane L < T
+  const uint32_t orow = L >> 4;
+  const bool rowact = ROWS && orow < T && item < n;
+  const uint32_t to = ROWS ? orow : o;
+  const bool tail_lane = ROWS ? rowact && (L & 15u) == 0u : L < T && item < n;
+  uint64_t* racc = (uint64_t*)(my + ITEM_WORDS) + (size_t)(orow < T ? orow : 0u) * lcv::FAN_COLS;
+  lcv::RowTabs rtabs;
+  if constexpr (ROWS) lcv::rw_tabs(rtabs);
+  // round r + 1's header and this lane's record words (its product's operand pair and scale; the tail's dst / io
+  // words; a row's dst, shadow and add-in words) are loaded at the top of round r, so their latency overlaps
+  // round r's work
+  // The round headers come one round earlier still (round r + 2's at the top of round r), through vector loads
+  // (an opaque zero lane offset keeps them off the scalar path), so the record addresses of round r + 1 do not
+  // wait on a header load: the vector loads of a wave complete in order, and a header's is older than the
+  // record loads of the round before it.
+  struct Hdr { uint32_t h0, off, words, h3; };
+  auto load_hdr = [&](uint32_t r) {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const uint32_t* p = f.P.hdr + 4 * r + z;
+    return Hdr{p[0], p[1], p[2], p[3]};
+  };
+  struct Rec { uint32_t h0, h3, x, y, m; lcv::SopPre pre; const uint32_t* w; uint32_t a0, a1, d0, d1; };
+  auto fetch = [&](const Hdr& hd) {
     Rec c;
-    c.h0 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r]);
-    const uint32_t off = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 1]);
-    const uint32_t words = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 2]);
-    c.h3 = __builtin_amdgcn_readfirstlane(f.P.hdr[4 * r + 3]);
+    c.h0 = __builtin_amdgcn_readfirstlane(hd.h0);
+    const uint32_t off = __builtin_amdgcn_readfirstlane(hd.off);
+    const uint32_t words = __builtin_amdgcn_readfirstlane(hd.words);
+    c.h3 = __builtin_amdgcn_readfirstlane(hd.h3);
     c.w = f.P.rec + off + o * words;
+    const uint32_t* wt = f.P.rec + off + (to < T ? to : 0u) * words;  // the tail's op's record
     const uint32_t K = c.h0 & 15u;
     c.x = c.y = c.m = 0;
     if (active && k < K) {
@@ -407,10 +437,20 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
       c.x = pw[0]; c.y = pw[1]; c.m = pw[2];
     }
     c.pre = lcv::SopPre{0, 0, 0, 0, 0};
-    if (L < T && item < n) c.pre = lcv::sop_pre(c.h0, c.w);
+    c.a0 = c.a1 = c.d0 = c.d1 = 0;
+    if (tail_lane) c.pre = lcv::sop_pre(c.h0, wt);
+    if (rowact) {
+      const uint32_t nadd = (c.h0 >> 4) & 3u;
+      c.d0 = wt[0];
+      c.d1 = wt[1];
+      if (nadd > 0) c.a0 = wt[2];
+      if (nadd > 1) c.a1 = wt[3];
+    }
     return c;
   };
-  Rec nx = fetch(0);
+  Hdr hn = load_hdr(0);
+  Rec nx = fetch(hn);
+  if (R > 1) hn = load_hdr(1);
 #if LCV_FAN_X_TIMING
   uint64_t tq[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tp = clock64();
 #define LCV_FAN_T(i) do { const uint64_t tn = clock64(); tq[i] += tn - tp; tp = tn; } while (0)
@@ -419,8 +459,19 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
 #endif
   for (uint32_t r = 0; r < R; ++r) {
     const Rec cur = nx;
-    if (r + 1 < R) nx = fetch(r + 1);
+    if (r + 1 < R) {
+      nx = fetch(hn);
+      if (r + 2 < R) hn = load_hdr(r + 2);
+    }
     const uint32_t h0 = cur.h0, K = h0 & 15u;
+    // a row's add-in terms are read now (the two words holding a lane's limb), before any tail of this round
+    // stores; the limbs are cut out in the tail, so the reads' latency overlaps the products
+    uint32_t tw[4] = {0, 0, 0, 0};
+    if (rowact) {
+      const uint32_t nadd = (h0 >> 4) & 3u;
+      if (nadd > 0) lcv::rw_limb_words(lcv::sop_src(cur.a0 & 0xFFFu, my, lds, ns), tw[0], tw[1]);
+      if (nadd > 1) lcv::rw_limb_words(lcv::sop_src(cur.a1 & 0xFFFu, my, lds, ns), tw[2], tw[3]);
+    }
     LCV_FAN_T(0);
     if (active && k < K) {
       if constexpr (S == 3) {
@@ -441,7 +492,48 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
     LCV_FAN_T(1);
     __syncthreads();
     LCV_FAN_T(2);
-    if (L < T && item < n) {  // op o's tail, in the first wave: every read of the round precedes its stores
+    if constexpr (ROWS) {
+      if (rowact) {  // K and the header flags are wave-uniform: the whole row takes one branch
+        uint32_t rl = 0;  // r = REDC(T): limb j on lane j (partly normalised)
+        if (K != 0) {
+          const uint32_t jj = L & 15u;
+          uint64_t lo = 0, hi = 0;
+          if (jj < 14u) {
+            lo = racc[jj];
+            hi = racc[jj + 14];
+            racc[jj] = 0;
+            racc[jj + 14] = 0;
+          }
+#if LCV_FAN_X_TIMING > 1
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          LCV_FAN_T(5);
+#endif
+          rl = lcv::rw_redc_limbs(lo, hi, rtabs);
+#if LCV_FAN_X_TIMING > 1
+          asm volatile("" :: "v"(rl));
+          LCV_FAN_T(6);
+#endif
+        }
+        const uint32_t vl = lcv::rw_value(rl, (h0 >> 4) & 3u, cur.a0, cur.a1, lcv::rw_limb_of(tw[0], tw[1]),
+                                          lcv::rw_limb_of(tw[2], tw[3]), (h0 >> 16) & 31u, rtabs);
+#if LCV_FAN_X_TIMING > 1
+        asm volatile("" :: "v"(vl));
+        LCV_FAN_T(7);
+#endif
+        if (h0 & ((1u << 10) | (1u << 11) | (1u << 12))) {  // inversion, side-load and emit rounds: on lane 0
+          uint32_t w[13];
+          lcv::rw_gather(w, lcv::rw_word(vl));
+          if (tail_lane) {
+            lcv::fp v;
+            w[12] = 0;
+            lcv::sop_tail_finish(v, h0 & ~(31u << 16), cur.pre, w, qp);  // (reduced already)
+            lcv::sop_tail_store(h0, cur.pre, my, io_in, io_out, v);
+          }
+        } else {
+          lcv::rw_store(vl, h0, cur.d0, cur.d1, my, rtabs);
+        }
+      }
+    } else if (tail_lane) {  // op o's tail, in the first wave: every read of the round precedes its stores
       uint32_t res[13];
       if (K == 0) {
         LCV_UNROLL for (int j = 0; j < 13; ++j) res[j] = 0;
@@ -466,20 +558,20 @@ __global__ __launch_bounds__(((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64
       LCV_FAN_T(7);
 #endif
       lcv::sop_tail_store(h0, cur.pre, my, io_in, io_out, v);
-#if LCV_FAN_X_TIMING > 1
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      LCV_FAN_T(8);
-#endif
     }
     LCV_FAN_T(3);
+#if LCV_FAN_X_TIMING > 1
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    LCV_FAN_T(8);
+#endif
     __syncthreads();
     LCV_FAN_T(4);
   }
 #if LCV_FAN_X_TIMING
   if (item == 0 && (L == 0 || L == NT - 64))
-    printf("fan T=%u KM=%u S=%u R=%u wave=%u: fetch %lu products %lu barrier1 %lu tail %lu barrier2 %lu | tail: "
-           "columns %lu redc %lu value %lu store %lu\n", T, KM, S, R, L / 64, tq[0], tq[1], tq[2], tq[3], tq[4], tq[5],
-           tq[6], tq[7], tq[8]);
+    printf("fan T=%u KM=%u S=%u R=%u rows=%d wave=%u: fetch %lu products %lu barrier1 %lu tail %lu barrier2 %lu | "
+           "tail: columns %lu redc %lu value %lu store %lu\n", T, KM, S, R, (int)ROWS, L / 64, tq[0], tq[1], tq[2], tq[3],
+           tq[4], tq[5], tq[6], tq[7], tq[8]);
 #endif
 #undef LCV_FAN_T
   if (L < T && item < n) f.epilogue(item, L, my);

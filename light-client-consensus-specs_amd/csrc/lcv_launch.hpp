@@ -76,10 +76,23 @@ template <class F> hipError_t lcv_hip_launch_sop(const F& f, uint32_t n, hipStre
   return hipGetLastError();
 }
 // the fan engine (latency mode, lcv_sop_fan.hpp): one item per block of TEAM x MAXK x F::FAN_PARTS lanes
-// (whole waves)
+// (whole waves), and at least 16 lanes per op when the ops' reductions run on rows of 16 lanes (LCV_FAN_ROW,
+// lcv_sop_row.hpp)
+#ifndef LCV_FAN_ROW
+#define LCV_FAN_ROW 1
+#endif
+#ifndef LCV_FAN_ROW_MAX_TEAM  // row tails for programs of at most this many ops a round (fexp 12, h2c 8; the
+#define LCV_FAN_ROW_MAX_TEAM 16  // fused Miller program's 32 rows would fill 8 waves: slower, profiles/r06_ab)
+#endif
+template <class F> constexpr bool lcv_fan_rows() { return LCV_FAN_ROW && F::TEAM <= LCV_FAN_ROW_MAX_TEAM; }
+template <class F> constexpr uint32_t lcv_fan_threads() {
+  constexpr uint32_t a = ((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64;
+  constexpr uint32_t b = lcv_fan_rows<F>() ? ((16 * F::TEAM + 63) / 64) * 64 : 0;
+  return a > b ? a : b;
+}
 template <class F> __global__ void k_sop_fan(F f, uint32_t n);
 template <class F> hipError_t lcv_hip_launch_sop_fan(const F& f, uint32_t n, hipStream_t s) {
-  constexpr uint32_t NT = ((F::TEAM * F::MAXK * F::FAN_PARTS + 63) / 64) * 64;
+  constexpr uint32_t NT = lcv_fan_threads<F>();
   const size_t lds_bytes = 4 * (size_t)(F::SHARED_WORDS + LCV_SOP_QP_WORDS + ((F::LDS_WORDS + 1u) & ~1u)) +
                            8 * (size_t)F::TEAM * 28;
   hipLaunchKernelGGL(k_sop_fan<F>, dim3(n), dim3(NT), lds_bytes, s, f, n);

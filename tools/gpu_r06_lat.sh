@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/r06_lat}
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_latency_gpu.py tests/test_golden_gpu.py tests/test_gpu_parity.py tests/test_wire.py tests/test_producer.py -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_row_tail_gpu.py tests/test_latency_gpu.py tests/test_golden_gpu.py tests/test_gpu_parity.py tests/test_wire.py tests/test_producer.py -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 OUT=$OUT bash tools/gpu_lat_ab.sh || exit 1
 if [ -n "${TIMING:-}" ]; then
