@@ -369,6 +369,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
 #ifndef LCV_FAN_X_TIMING
 #define LCV_FAN_X_TIMING 0
 #endif
+#ifndef LCV_FAN_X_NOATOMIC
+#define LCV_FAN_X_NOATOMIC 0
+#endif
 // LCV_FAN_ROW (lcv_launch.hpp, the default) for the programs of at most LCV_FAN_ROW_MAX_TEAM ops a round
 // (lcv_fan_rows<F>: the final exponentiation and hash_to_G2's tail): op o's tail runs on the 16-lane row of lanes
 // 16 o .. 16 o + 15 (lcv_sop_row.hpp: the reduction as two column passes, one column pair per lane; the add-ins,
@@ -478,9 +481,14 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
       int64_t c13[13];
       lcv::sop_fan_part(c13, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, part, base);
       const uint32_t at = part == 0 ? 0u : (part == 1 ? 14u : 7u);
+#if LCV_FAN_X_NOATOMIC  // timing experiment only (wrong results): one atomic per lane instead of 13 or 26
+      { uint64_t xs = 0; LCV_UNROLL for (int c = 0; c < 13; ++c) xs ^= (uint64_t)c13[c];
+        __hip_atomic_fetch_add(acc + at, xs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+      if (false)
+#endif
       LCV_UNROLL for (int c = 0; c < 13; ++c)
         __hip_atomic_fetch_add(acc + at + c, (uint64_t)c13[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (part != 2)
+      if (part != 2 && !LCV_FAN_X_NOATOMIC)
         LCV_UNROLL for (int c = 0; c < 13; ++c)
           __hip_atomic_fetch_add(acc + 7 + c, (uint64_t)c13[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
