@@ -151,12 +151,12 @@ int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
  * bls.FastAggregateVerify once per update, sync-protocol.md:512, :464): calls whose batch (or chunk) has
  * at most max_rows rows run
  *   - the SOP programs (hash_to_G2 tail, final exponentiation) on the fan engine — an op's K products on
- *     K lanes, one update per block — instead of one op per lane,
+ *     K lanes and its reduction and tail on a 16-lane row, one update per block — instead of one op per lane,
  *   - both Miller line walks and the accumulation as ONE fan-engine program (lines through LDS), and
  *   - the SSWU maps and the signature decoding on their one-item-per-wave twins (each square-root
  *     product spread over the 64 lanes of a wave).
- * Results are identical to the batch engine's (bit for bit).  Default 64: one update 3.2 ms through
- * lcv_validate_updates on the MI355X (6.1 ms on the batch engine); 0 = the batch engine
+ * Results are identical to the batch engine's (bit for bit).  Default 64: one update 3.0 ms through
+ * lcv_validate_updates on the MI355X (5.9 ms on the batch engine); 0 = the batch engine
  * always.  Performance knob only. */
 int lcv_set_latency_mode(lcv_ctx* ctx, uint64_t max_rows);
 /* test hook: which engines ran since the last reset (reset != 0 clears after reading).  out8[0] fan-engine

@@ -147,10 +147,10 @@ class Verifier:
 
     def set_latency_mode(self, max_rows: int) -> None:
         """Latency mode for small batches (lcv_set_latency_mode): batches of at most max_rows rows run the SOP
-        programs (hash_to_G2's tail, final exponentiation) on the fan engine (an op's K products on K lanes,
-        one item per block), both Miller walks and the accumulation as one fan-engine program, and the SSWU
+        programs (hash_to_G2's tail, final exponentiation) on the fan engine (an op's K products on K lanes, its
+        reduction and tail on a 16-lane row, one item per block), both Miller walks and the accumulation as one fan-engine program, and the SSWU
         maps / signature decoding one item per wave (square-root chains spread over the wave) — one update
-        6.1 ms on the batch engine -> 3.2 ms.  Results are identical to the batch engine's.  Default 64;
+        5.9 ms on the batch engine -> 3.0 ms.  Results are identical to the batch engine's.  Default 64;
         0 = the batch engine always."""
         self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
         self.latency_mode = int(max_rows)
