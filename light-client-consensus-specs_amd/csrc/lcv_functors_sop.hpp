@@ -441,7 +441,7 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
     }
     c.pre = lcv::SopPre{0, 0, 0, 0, 0};
     c.a0 = c.a1 = c.d0 = c.d1 = 0;
-    if (tail_lane) c.pre = lcv::sop_pre(c.h0, wt);
+    if (tail_lane && !ROWS) c.pre = lcv::sop_pre(c.h0, wt);  // (rows: the dst / io words are d0 / d1 below)
     if (rowact) {
       const uint32_t nadd = (c.h0 >> 4) & 3u;
       c.d0 = wt[0];
@@ -534,8 +534,9 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
           if (tail_lane) {
             lcv::fp v;
             w[12] = 0;
-            lcv::sop_tail_finish(v, h0 & ~(31u << 16), cur.pre, w, qp);  // (reduced already)
-            lcv::sop_tail_store(h0, cur.pre, my, io_in, io_out, v);
+            const lcv::SopPre pre{cur.d0, cur.d1, 0, 0, 0};
+            lcv::sop_tail_finish(v, h0 & ~(31u << 16), pre, w, qp);  // (reduced already)
+            lcv::sop_tail_store(h0, pre, my, io_in, io_out, v);
           }
         } else {
           lcv::rw_store(vl, h0, cur.d0, cur.d1, my, rtabs);
