@@ -47,15 +47,18 @@ LCV_FN uint32_t rw_j() { return __lane_id() & 15u; }
 
 // per-lane tables (lane j of a row): nq[i] = n_(j-i) for i <= j < 14 (n = -p^-1 mod 2^392, 28-bit limbs);
 // pl[i] = p_(j-i) for i <= j < 14; ph[i] = p_(j+14-i) for j < i (the column pass's low / high column terms)
-struct RowTabs { uint32_t nq[14], pl[14], ph[14], pj; };  // pj: p's limb j (0 on lanes 14, 15)
+struct RowTabs { uint32_t nq[14], pl[14], ph[14], pj, pw; };  // pj: p's limb j (0 on lanes 14, 15); pw: p's word j
 LCV_FN void rw_tabs(RowTabs& T) {
   constexpr uint32_t NQ[14] = LCV_NP392_L28_INIT;
+  constexpr uint32_t PW[12] = LCV_P_INIT;
   const uint32_t j = rw_j();
-  uint32_t n = 0, p = 0;
+  uint32_t n = 0, p = 0, w = 0;
   LCV_UNROLL for (int i = 0; i < 14; ++i) {
     n = j == (uint32_t)i ? NQ[i] : n;
     p = j == (uint32_t)i ? kP28.v[i] : p;
+    if (i < 12) w = j == (uint32_t)i ? PW[i] : w;
   }
+  T.pw = w;
   const uint32_t lo = j < 14u ? 0xFFFFFFFFu : 0u;
   T.pj = p;
   T.nq[0] = n;
@@ -243,6 +246,17 @@ LCV_FN uint32_t rw_value(uint32_t rl, uint32_t nadd, uint32_t a0, uint32_t a1, u
   }
   return (uint32_t)x & (j < 14u ? 0xFFFFFFFFu : 0u);
 }
+// p - v as words (v < p, word w on lane w < 12; p's word from the table): per-word differences and a borrow
+// lookahead over two row ballots — generate p_w < v_w, propagate p_w == v_w: the borrows are the carries of
+// (G | P) + G, as in rw_norm_exact
+LCV_FN uint32_t rw_neg_word(uint32_t vw, uint32_t pw) {
+  const uint32_t j = rw_j();
+  const bool act = j < 12u;
+  const uint32_t g = rw_bits(__builtin_amdgcn_ballot_w64(act && pw < vw));
+  const uint32_t pr = rw_bits(__builtin_amdgcn_ballot_w64(act && pw == vw));
+  const uint32_t a = g | pr, bin = (((a + g) ^ a ^ g) >> j) & 1u;
+  return pw - vw - bin;
+}
 // v's store on its row (sop_tail_store without side-loads / emits, which take the gathered path): lane w < 12
 // writes word w of v to the destination slot and of p - v to its shadow; r0 / r1 are the op's record words 0 / 1
 LCV_FN void rw_store(uint32_t vl, uint32_t h0, uint32_t r0, uint32_t r1, uint32_t* wr, const RowTabs& T) {
@@ -252,8 +266,7 @@ LCV_FN void rw_store(uint32_t vl, uint32_t h0, uint32_t r0, uint32_t r1, uint32_
   const uint32_t word = rw_word(vl);
   if (j < 12u) wr[12u * dst + j] = word;
   if (((h0 >> 13) & 1u) && dsh != 0x3FFu) {  // shadow: p - v in (0, p]
-    const uint32_t sl = (uint32_t)rw_norm_exact_s(rw_norm2s(rw_biased_sub(T.pj, vl)));
-    const uint32_t sw = rw_word(sl);
+    const uint32_t sw = rw_neg_word(word, T.pw);
     if (j < 12u) wr[12u * dsh + j] = sw;
   }
 }
