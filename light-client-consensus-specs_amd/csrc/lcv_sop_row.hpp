@@ -184,9 +184,10 @@ LCV_FN uint32_t rw_redc_limbs(uint64_t lo, uint64_t hi, const RowTabs& T) {
   uint64_t R = hn << 8;
   if (j == 0) R += ((uint64_t)(u13 + e) >> 20) + ((uint64_t)u14 << 8);
   if (j == 1) R += (uint64_t)u15 << 8;
-  // partly normalised (lanes 0..13 below 2^28 + 2^9; lanes 14, 15 zero: the limbs are non-negative and r' < 2^391);
-  // rw_value normalises exactly once, after the add-ins and the reduction
-  return (uint32_t)rw_norm2(R);
+  // partly normalised by one carry round (R's limbs are below 2^37: lanes 0..13 end below 2^28 + 2^9; lanes 14, 15
+  // zero: the limbs are non-negative and r' < 2^391); rw_value normalises exactly once, after the add-ins and the
+  // reduction
+  return (uint32_t)((R & SOP_M28) + rw_shr1_64(R >> 28));
 }
 
 // The rest of the op's tail on its row: from r's limbs (lanes 0..13 in [0, 2^28 + 2^9], rw_redc_limbs) to
