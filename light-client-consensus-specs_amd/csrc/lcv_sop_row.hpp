@@ -91,17 +91,11 @@ LCV_FN uint32_t rw_norm_exact(uint32_t x) {
   return (x + (cin & 1u)) & SOP_M28;
 }
 
-// signed rows (the tail's add-in, reduction and shadow steps): two carry rounds over lanes 0..13 into lane 14,
-// the row's signed top limb (it holds the bias terms' compensation, below), which is never masked and carries
-// nothing on; lanes 0..13 hold non-negative values here
-LCV_FN int64_t rw_norm2s(int64_t x) {
-  const bool low = rw_j() < 14u;
-  LCV_UNROLL for (int k = 0; k < 2; ++k)
-    x = (low ? (x & SOP_M28) : x) + (int64_t)rw_shr1_64(low ? (uint64_t)(x >> 28) : 0ull);
-  return x;
-}
-// exact: lanes 0..13 in [0, 2^28 + 2^9] (after rw_norm2s of a value whose limbs 0..13 are non-negative) become
-// canonical, lane 14 (signed) receives their carry; the carry-lookahead of rw_norm_exact
+// signed rows (the tail's add-in and reduction steps): lanes 0..13 hold non-negative limbs, lane 14 a signed top limb
+// (it receives the bias terms' compensation, below) that is never masked and carries nothing on
+// exact: lanes 0..13 in [0, 2^29) (non-negative limbs after at most one carry round, or a biased difference) become
+// canonical, lane 14 (signed) receives their carry: its own carry round leaves limbs <= 2^28, whose carries (0 or 1)
+// the carry-lookahead of rw_norm_exact resolves
 LCV_FN int64_t rw_norm_exact_s(int64_t x) {
   const uint32_t j = rw_j();
   const bool low = j < 14u;
@@ -199,7 +193,7 @@ LCV_FN uint32_t rw_redc_limbs(uint64_t lo, uint64_t hi, const RowTabs& T) {
 // and its exactness test (a fractional part of e at most 1 - 2^-29 proves q exact); x - q p (biased, lanes
 // non-negative) is then normalised exactly once.  Only an inexact estimate (~2^-29 of the ops; row-uniform)
 // takes the conditional subtraction of p, decided by the biased difference's lane 14.  v's limb on lane j.
-LCV_FN int64_t rw_carry1s(int64_t x) {  // one carry round over lanes 0..13 into lane 14 (see rw_norm2s)
+LCV_FN int64_t rw_carry1s(int64_t x) {  // one carry round over lanes 0..13 into lane 14 (signed rows)
   const bool low = rw_j() < 14u;
   return (low ? (x & SOP_M28) : x) + (int64_t)rw_shr1_64(low ? (uint64_t)(x >> 28) : 0ull);
 }
@@ -233,15 +227,15 @@ LCV_FN uint32_t rw_value(uint32_t rl, uint32_t nadd, uint32_t a0, uint32_t a1, u
     exact = false;
 #endif
     int64_t y = x - q * (int64_t)pj + (j < 14u ? q << 28 : 0) - ((j >= 1u && j <= 14u) ? q : 0);
-    y = rw_norm_exact_s(rw_norm2s(y));  // x - q p: in [0, p) when exact, else in [0, 2p)
+    y = rw_norm_exact_s(rw_carry1s(y));  // x - q p: in [0, p) when exact, else in [0, 2p) (limbs < 2^44: one round)
     if (__builtin_expect(!exact, 0)) {
-      const int64_t z = rw_norm_exact_s(rw_norm2s(rw_biased_sub((uint32_t)y, pj)));
+      const int64_t z = rw_norm_exact_s(rw_biased_sub((uint32_t)y, pj));  // (biased limbs < 2^29)
       const bool ge = (int32_t)rw_bcast<14>((uint32_t)z) == 0;  // y >= p
       y = ge ? z : y;
     }
     x = y;
   } else if (nadd) {
-    x = rw_norm_exact_s(rw_norm2s(x));
+    x = rw_norm_exact_s(rw_carry1s(x));  // (limbs below 2^28 + 2^9 + 2^29 sum |c| < 2^45: one round)
   } else {
     x = rw_norm_exact(rl);
   }
