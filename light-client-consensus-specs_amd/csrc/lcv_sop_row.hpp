@@ -11,8 +11,8 @@
 //        sop_redc28's digits spell;
 //   T + M p as a second column pass (lane j: column j and column j + 14);
 //   r' from the columns: the low half's carry across bit 384 is (u13 + [u0..u12 not all zero]) >> 20 (its low
-//        384 bits are zero and every partly normalised limb is below 2^28 + 2^9), the high half partly normalised
-//        and moved up 8 bits (2^392 = 2^8 2^384).
+//        384 bits are zero and every partly normalised limb is below 2^28 + 2^9), the high half after one carry
+//        round moved up 8 bits (2^392 = 2^8 2^384) and carried once more.
 // So r' = (T + M p) / 2^384 is sop_redc28's r as a value (limbs partly normalised); the rest of the op's tail runs on
 // the row too (rw_value: the add-in terms, the quotient estimate from the top limbs, one exact normalisation — two
 // carry rounds, then a carry-lookahead over two row ballots: generate = limb 2^28, propagate = limb 2^28 - 1; rw_store:
@@ -80,12 +80,11 @@ LCV_FN uint64_t rw_norm2(uint64_t x) {
 }
 // the row's 16 bits of a wave ballot
 LCV_FN uint32_t rw_bits(uint64_t ballot) { return (uint32_t)(ballot >> (__lane_id() & 48u)) & 0xFFFFu; }
-// exact normalisation of limbs in [0, 2^28 + 2^9] (lanes 0..13; lanes 14, 15 zero): a third carry round leaves
-// limbs in [0, 2^28], whose carries (0 or 1) a lookahead resolves: carry into lane j+1 = g_j | (p_j & carry_j)
-// with g = (limb == 2^28), p = (limb == 2^28 - 1): the carries of the addition (G | P) + G
+// exact normalisation of limbs below 2^29 - 1 (lanes 0..13; lanes 14, 15 zero): limb + carry-in stays below 2^29,
+// so every carry is 0 or 1 and a lookahead resolves them at once: carry into lane j+1 = g_j | (p_j & carry_j) with
+// g = (limb >= 2^28), p = (limb == 2^28 - 1) — the carries of the addition (G | P) + G
 LCV_FN uint32_t rw_norm_exact(uint32_t x) {
-  x = (x & SOP_M28) + rw_shr1(x >> 28);
-  const uint32_t g = rw_bits(__builtin_amdgcn_ballot_w64(x == (1u << 28)));
+  const uint32_t g = rw_bits(__builtin_amdgcn_ballot_w64(x > SOP_M28));
   const uint32_t pr = rw_bits(__builtin_amdgcn_ballot_w64(x == SOP_M28));
   const uint32_t a = g | pr, cin = ((a + g) ^ a ^ g) >> rw_j();
   return (x + (cin & 1u)) & SOP_M28;
@@ -93,14 +92,12 @@ LCV_FN uint32_t rw_norm_exact(uint32_t x) {
 
 // signed rows (the tail's add-in and reduction steps): lanes 0..13 hold non-negative limbs, lane 14 a signed top limb
 // (it receives the bias terms' compensation, below) that is never masked and carries nothing on
-// exact: lanes 0..13 in [0, 2^29) (non-negative limbs after at most one carry round, or a biased difference) become
-// canonical, lane 14 (signed) receives their carry: its own carry round leaves limbs <= 2^28, whose carries (0 or 1)
-// the carry-lookahead of rw_norm_exact resolves
+// exact: lanes 0..13 in [0, 2^29 - 1) (non-negative limbs after a carry round, or a biased difference) become
+// canonical, lane 14 (signed) receives their carry: the carry-lookahead of rw_norm_exact
 LCV_FN int64_t rw_norm_exact_s(int64_t x) {
   const uint32_t j = rw_j();
   const bool low = j < 14u;
-  x = (low ? (x & SOP_M28) : x) + (int64_t)rw_shr1_64(low ? (uint64_t)(x >> 28) : 0ull);
-  const uint32_t g = rw_bits(__builtin_amdgcn_ballot_w64(low && x == (int64_t)(1u << 28)));
+  const uint32_t g = rw_bits(__builtin_amdgcn_ballot_w64(low && x > (int64_t)SOP_M28));
   const uint32_t pr = rw_bits(__builtin_amdgcn_ballot_w64(low && x == (int64_t)SOP_M28));
   const uint32_t a = g | pr, cin = (((a + g) ^ a ^ g) >> j) & 1u;
   return low ? ((x + cin) & SOP_M28) : x + cin;
@@ -173,18 +170,19 @@ LCV_FN uint32_t rw_redc_limbs(uint64_t lo, uint64_t hi, const RowTabs& T) {
   const uint32_t u = (uint32_t)rw_norm2(l0 + l1);
   const uint32_t e = (rw_bits(__builtin_amdgcn_ballot_w64(j < 13u && u != 0u)) & 0x1FFFu) != 0u ? 1u : 0u;
   const uint32_t u13 = rw_bcast<13>(u), u14 = rw_bcast<14>(u), u15 = rw_bcast<15>(u);
-  // high half (relative to 2^392): normalised, moved up 8 bits; r' < 2^391, so its lanes 14, 15 are zero
-  const uint64_t hn = rw_norm2(h0 + h1);
+  // high half (relative to 2^392): one carry round (limbs below 2^28 + 2^36), moved up 8 bits; r' < 2^391 and the
+  // limbs are non-negative, so its lanes 14, 15 are zero
+  const uint64_t hs = h0 + h1, hn = (hs & SOP_M28) + rw_shr1_64(hs >> 28);
   uint64_t R = hn << 8;
   if (j == 0) R += ((uint64_t)(u13 + e) >> 20) + ((uint64_t)u14 << 8);
   if (j == 1) R += (uint64_t)u15 << 8;
-  // partly normalised by one carry round (R's limbs are below 2^37: lanes 0..13 end below 2^28 + 2^9; lanes 14, 15
+  // partly normalised by one carry round (R's limbs are below 2^45: lanes 0..13 end below 2^28 + 2^17; lanes 14, 15
   // zero: the limbs are non-negative and r' < 2^391); rw_value normalises exactly once, after the add-ins and the
   // reduction
   return (uint32_t)((R & SOP_M28) + rw_shr1_64(R >> 28));
 }
 
-// The rest of the op's tail on its row: from r's limbs (lanes 0..13 in [0, 2^28 + 2^9], rw_redc_limbs) to
+// The rest of the op's tail on its row: from r's limbs (lanes 0..13 in [0, 2^28 + 2^17), rw_redc_limbs) to
 // v = (r + sum |c| u) mod p canonical, the value sop_tail_value stores (u = the add-in slot's value, or p - it for
 // c < 0; the terms' limbs tl0 / tl1 were read from LDS at the top of the round).  The terms are multiply-adds per
 // lane (a negative one as |c| times the biased p - u).  For red > 0 (x < 2^red p, the header's bound) the quotient
@@ -235,7 +233,7 @@ LCV_FN uint32_t rw_value(uint32_t rl, uint32_t nadd, uint32_t a0, uint32_t a1, u
     }
     x = y;
   } else if (nadd) {
-    x = rw_norm_exact_s(rw_carry1s(x));  // (limbs below 2^28 + 2^9 + 2^29 sum |c| < 2^45: one round)
+    x = rw_norm_exact_s(rw_carry1s(x));  // (limbs below 2^28 + 2^17 + 2^29 sum |c| < 2^45: one round)
   } else {
     x = rw_norm_exact(rl);
   }
