@@ -2,9 +2,10 @@
 // lcv_functors_sop.hpp k_sop_fan with LCV_FAN_ROW): one op's 28 column sums, lane j holding columns j and
 // j + 14, instead of one lane running sop_redc28's 196 multiply-adds back to back.
 //
-// A lone wave is bound by instruction issue in sop_redc28 (~6 shader cycles per wave64 multiply-add at one
-// wave per SIMD, tools/microbench/peakbench.hip: 1,850 of a final-exponentiation round's ~7,000 cycles,
-// profiles/r06_ab/tail_timing_A.txt), so the row form cuts the instructions on the tail's wave: per lane
+// A lone wave is bound by instruction issue in sop_redc28 (4.2-4.8 shader cycles per wave64 instruction at one wave
+// per SIMD, DPP moves and 64-bit multiply-adds alike, chained or not: tools/microbench/dppbench.hip; 1,850 of a
+// final-exponentiation round's ~7,000 cycles, profiles/r06_ab/tail_timing_A.txt), so the row form cuts the
+// instructions on the tail's wave: per lane
 //   t  = T mod 2^392, partly normalised (two carry rounds: limbs < 2^28 + 2^9, value kept);
 //   M  = t (-p^-1) mod 2^384 as a column pass (14 row broadcasts + multiply-adds), normalised exactly and cut
 //        to 384 bits: the canonical Montgomery quotient (M < 2^384, T + M p = 0 mod 2^384), the one
@@ -14,9 +15,10 @@
 //        384 bits are zero and every partly normalised limb is below 2^28 + 2^9), the high half after one carry
 //        round moved up 8 bits (2^392 = 2^8 2^384) and carried once more.
 // So r' = (T + M p) / 2^384 is sop_redc28's r as a value (limbs partly normalised); the rest of the op's tail runs on
-// the row too (rw_value: the add-in terms, the quotient estimate from the top limbs, one exact normalisation — two
-// carry rounds, then a carry-lookahead over two row ballots: generate = limb 2^28, propagate = limb 2^28 - 1; rw_store:
-// the value's and its shadow's words, one per lane).  Bit for bit sop_tail_value + sop_tail_store:
+// the row too (rw_value: the add-in terms, the quotient estimate from the top limbs, one exact normalisation — a
+// carry round, then a carry-lookahead over two row ballots: generate = limb >= 2^28, propagate = limb 2^28 - 1;
+// rw_store: the value's words and its shadow's, p - v by a borrow lookahead, one word per lane).  Bit for bit
+// sop_tail_value + sop_tail_store:
 // tools/microbench/rowtest.hip.  Row lanes 14 and 15 hold zeros (lane 14: a signed top limb in the tail's steps).
 // Device-only (DPP row_newbcast / row_shr / row_shl within 16-lane rows, gfx90a+).
 #pragma once
