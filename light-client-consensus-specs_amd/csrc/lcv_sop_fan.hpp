@@ -28,6 +28,9 @@
 #ifndef LCV_FAN_SPLIT
 #define LCV_FAN_SPLIT 1
 #endif
+#ifndef LCV_FAN_X_CUT  // timing experiments only: 1 no operand reads, 2 no conversion, 3 no multiply-adds
+#define LCV_FAN_X_CUT 0
+#endif
 #ifndef LCV_FAN_PARTS
 #define LCV_FAN_PARTS (LCV_FAN_SPLIT ? 3u : 1u)
 #endif
@@ -64,8 +67,12 @@ LCV_FN void sop_fan_product(uint64_t col[28], uint32_t xw, uint32_t yw, uint32_t
 LCV_FN void sop_fan_part(int64_t c[13], uint32_t xw, uint32_t yw, uint32_t mk, uint32_t k, uint32_t masks,
                          bool mflag, uint32_t part, const SopBase& base) {
   uint32_t Xw[13], Yw[12], X[15], Y[14];
+#if LCV_FAN_X_CUT == 1  // timing experiments only (wrong results): no operand reads
+  LCV_UNROLL for (int j = 0; j < 12; ++j) { Xw[j] = xw * (j + 1); Yw[j] = yw + j; }
+#else
   sop_operand(Xw, xw, (masks >> k) & 1u, base);
   sop_operand(Yw, yw, (masks >> (16 + k)) & 1u, base);
+#endif
   Xw[12] = 0;
   if (mflag) {  // X *= m (m < 2^16): 13 words
     uint32_t carry = 0;
@@ -76,6 +83,11 @@ LCV_FN void sop_fan_part(int64_t c[13], uint32_t xw, uint32_t yw, uint32_t mk, u
     }
     Xw[12] = carry;
   }
+#if LCV_FAN_X_CUT == 2  // no conversion or part selection: words as limbs
+  int32_t a[7], b[7];
+  LCV_UNROLL for (int i = 0; i < 7; ++i) { a[i] = (int32_t)(Xw[i + part] & SOP_M28); b[i] = (int32_t)(Yw[i + part] & SOP_M28); }
+  (void)X; (void)Y;
+#else
   sop_to28<12, 14>(Y, Yw);
   sop_to28<13, 14>(X, Xw);
   int32_t a[7], b[7];
@@ -85,7 +97,12 @@ LCV_FN void sop_fan_part(int64_t c[13], uint32_t xw, uint32_t yw, uint32_t mk, u
     a[i] = p0 ? xl : (p1 ? xh : xl - xh);
     b[i] = p0 ? yl : (p1 ? yh : yh - yl);
   }
+#endif
+#if LCV_FAN_X_CUT == 3  // no multiply-adds: the inputs as columns
+  LCV_UNROLL for (int i = 0; i < 13; ++i) c[i] = (int64_t)a[i % 7] + b[(i + 3) % 7];
+#else
   sop_mac7s<true>(c, a, b);
+#endif
 }
 
 }  // namespace lcv
