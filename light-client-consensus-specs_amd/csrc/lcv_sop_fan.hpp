@@ -28,7 +28,7 @@
 #ifndef LCV_FAN_SPLIT
 #define LCV_FAN_SPLIT 1
 #endif
-#ifndef LCV_FAN_X_CUT  // timing experiments only: 1 no operand reads, 2 no conversion, 3 no multiply-adds
+#ifndef LCV_FAN_X_CUT  // timing experiments only: 1 no operand reads, 2 no conversion, 3 no multiply-adds, 4 limb-form operands
 #define LCV_FAN_X_CUT 0
 #endif
 #ifndef LCV_FAN_PARTS
@@ -67,6 +67,33 @@ LCV_FN void sop_fan_product(uint64_t col[28], uint32_t xw, uint32_t yw, uint32_t
 LCV_FN void sop_fan_part(int64_t c[13], uint32_t xw, uint32_t yw, uint32_t mk, uint32_t k, uint32_t masks,
                          bool mflag, uint32_t part, const SopBase& base) {
   uint32_t Xw[13], Yw[12], X[15], Y[14];
+#if LCV_FAN_X_CUT == 4  // timing: operands as if stored as 28-bit limbs (16 words a slot; wrong results)
+  {
+    uint32_t La[16], Lb[16];
+    const uint32_t* pa = sop_pterm(xw & 0xFFFFu, base);
+    LCV_UNROLL for (int j = 0; j < 16; ++j) La[j] = pa[j];
+    if ((masks >> k) & 1u) {
+      const uint32_t* pb = sop_pterm(xw >> 16, base);
+      LCV_UNROLL for (int j = 0; j < 16; ++j) La[j] += pb[j];
+    }
+    const uint32_t* qa = sop_pterm(yw & 0xFFFFu, base);
+    LCV_UNROLL for (int j = 0; j < 16; ++j) Lb[j] = qa[j];
+    if ((masks >> (16 + k)) & 1u) {
+      const uint32_t* qb = sop_pterm(yw >> 16, base);
+      LCV_UNROLL for (int j = 0; j < 16; ++j) Lb[j] += qb[j];
+    }
+    int32_t a[7], b[7];
+    const bool p0 = part == 0, p1 = part == 1;
+    LCV_UNROLL for (int i = 0; i < 7; ++i) {
+      const int32_t xl = (int32_t)La[i], xh = (int32_t)La[i + 7], yl = (int32_t)Lb[i], yh = (int32_t)Lb[i + 7];
+      a[i] = p0 ? xl : (p1 ? xh : xl - xh);
+      b[i] = p0 ? yl : (p1 ? yh : yh - yl);
+    }
+    sop_mac7s<true>(c, a, b);
+    (void)mflag; (void)mk; (void)Xw; (void)Yw; (void)X; (void)Y;
+    return;
+  }
+#endif
 #if LCV_FAN_X_CUT == 1  // timing experiments only (wrong results): no operand reads
   LCV_UNROLL for (int j = 0; j < 12; ++j) { Xw[j] = xw * (j + 1); Yw[j] = yw + j; }
 #else
