@@ -467,14 +467,6 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
       if (r + 2 < R) hn = load_hdr(r + 2);
     }
     const uint32_t h0 = cur.h0, K = h0 & 15u;
-    // a row's add-in terms are read now (the two words holding a lane's limb), before any tail of this round
-    // stores; the limbs are cut out in the tail, so the reads' latency overlaps the products
-    uint32_t tw[4] = {0, 0, 0, 0};
-    if (rowact) {
-      const uint32_t nadd = (h0 >> 4) & 3u;
-      if (nadd > 0) lcv::rw_limb_words(lcv::sop_src(cur.a0 & 0xFFFu, my, lds, ns), tw[0], tw[1]);
-      if (nadd > 1) lcv::rw_limb_words(lcv::sop_src(cur.a1 & 0xFFFu, my, lds, ns), tw[2], tw[3]);
-    }
     LCV_FAN_T(0);
     if (active && k < K) {
       if constexpr (S == 3) {
@@ -496,6 +488,14 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
       lcv::sop_fan_product(col, cur.x, cur.y, cur.m, k, cur.h3, (h0 >> 6) & 1u, base);
       LCV_UNROLL for (int c = 0; c < 28; ++c) __hip_atomic_fetch_add(acc + c, col[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+    }
+    // a row's add-in terms are read now (the two words holding a lane's limb): after the products' operand reads and
+    // before the barrier, so before any tail of this round stores; the limbs are cut out in the tail
+    uint32_t tw[4] = {0, 0, 0, 0};
+    if (rowact) {
+      const uint32_t nadd = (h0 >> 4) & 3u;
+      if (nadd > 0) lcv::rw_limb_words(lcv::sop_src(cur.a0 & 0xFFFu, my, lds, ns), tw[0], tw[1]);
+      if (nadd > 1) lcv::rw_limb_words(lcv::sop_src(cur.a1 & 0xFFFu, my, lds, ns), tw[2], tw[3]);
     }
     LCV_FAN_T(1);
     __syncthreads();
