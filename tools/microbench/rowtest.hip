@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64) void k_rowtest(const Op* ops, uint32_t nops, ui
   const bool none = id % 8 == 6;
   const uint32_t r0 = none ? (uint32_t)lcv::SOP_SLOT_NONE : 0u, r1 = none ? 0u : 1u << 12;
   uint32_t rw[13], vw[13];
-  lcv::rw_gather(rw, lcv::rw_word(rl));
+  lcv::rw_gather(rw, lcv::rw_word(lcv::rw_norm_exact(rl)));  // (rl: partly normalised limbs)
   lcv::rw_gather(vw, lcv::rw_word(vl));
   lcv::rw_store(vl, h0, r0, r1, &wr[row][0][0], T);
   __syncthreads();
