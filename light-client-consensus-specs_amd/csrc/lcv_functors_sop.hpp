@@ -369,6 +369,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
 #ifndef LCV_FAN_X_TIMING
 #define LCV_FAN_X_TIMING 0
 #endif
+#ifndef LCV_FAN_FLAT_FETCH
+#define LCV_FAN_FLAT_FETCH 1
+#endif
+#ifndef LCV_FAN_LATE_FETCH
+#define LCV_FAN_LATE_FETCH 1
+#endif
 #ifndef LCV_FAN_X_NOATOMIC
 #define LCV_FAN_X_NOATOMIC 0
 #endif
@@ -434,6 +440,20 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
     c.w = f.P.rec + off + o * words;
     const uint32_t* wt = f.P.rec + off + (to < T ? to : 0u) * words;  // the tail's op's record
     const uint32_t K = c.h0 & 15u;
+#if LCV_FAN_FLAT_FETCH
+    // branch-free: every lane loads (a lone wave pays each exec-mask region and branch in series).  Product k is
+    // clamped into op o's record (4 + 3 K words: its first words when K = 0); the values are used only by the lanes
+    // they belong to (active, k < K; a row's add-in words only when the header counts them)
+    const uint32_t kk = k < K ? k : (K ? K - 1u : 0u);
+    const uint32_t* pw = c.w + (K ? 4u + 3u * kk : 0u);
+    c.x = pw[0]; c.y = pw[1]; c.m = pw[2];
+    c.pre = lcv::SopPre{0, 0, 0, 0, 0};
+    if (!ROWS && tail_lane) c.pre = lcv::sop_pre(c.h0, wt);
+    c.d0 = c.d1 = c.a0 = c.a1 = 0;
+    if constexpr (ROWS) {
+      c.d0 = wt[0]; c.d1 = wt[1]; c.a0 = wt[2]; c.a1 = wt[3];
+    }
+#else
     c.x = c.y = c.m = 0;
     if (active && k < K) {
       const uint32_t* pw = c.w + 4 + 3 * k;
@@ -449,6 +469,7 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
       if (nadd > 0) c.a0 = wt[2];
       if (nadd > 1) c.a1 = wt[3];
     }
+#endif
     return c;
   };
   Hdr hn = load_hdr(0);
@@ -460,12 +481,15 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
 #else
 #define LCV_FAN_T(i) ((void)0)
 #endif
-  for (uint32_t r = 0; r < R; ++r) {
-    const Rec cur = nx;
+  auto prefetch = [&](uint32_t r) {
     if (r + 1 < R) {
       nx = fetch(hn);
       if (r + 2 < R) hn = load_hdr(r + 2);
     }
+  };
+  for (uint32_t r = 0; r < R; ++r) {
+    const Rec cur = nx;
+    if (!LCV_FAN_LATE_FETCH) prefetch(r);
     const uint32_t h0 = cur.h0, K = h0 & 15u;
     LCV_FAN_T(0);
     if (active && k < K) {
@@ -497,6 +521,10 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
       if (nadd > 0) lcv::rw_limb_words(lcv::sop_src(cur.a0 & 0xFFFu, my, lds, ns), tw[0], tw[1]);
       if (nadd > 1) lcv::rw_limb_words(lcv::sop_src(cur.a1 & 0xFFFu, my, lds, ns), tw[2], tw[3]);
     }
+    // LCV_FAN_LATE_FETCH: round r + 1's record loads (and round r + 2's header) are issued here, while the column
+    // atomics drain before the barrier (it waits on LDS only), instead of at the top of the round, where a lone wave
+    // pays their issue in series with its products; they are still a whole tail ahead of their use
+    if (LCV_FAN_LATE_FETCH) prefetch(r);
     LCV_FAN_T(1);
     __syncthreads();
     LCV_FAN_T(2);
