@@ -481,15 +481,15 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
 #else
 #define LCV_FAN_T(i) ((void)0)
 #endif
-  auto prefetch = [&](uint32_t r) {
-    if (r + 1 < R) {
-      nx = fetch(hn);
-      if (r + 2 < R) hn = load_hdr(r + 2);
-    }
+  // round r reads its record `cur` and fetches round r + 1's into `nxr` (unconditionally: past the last round it
+  // re-reads the last round's record).  The loop runs two rounds a trip with the two records swapping roles, so
+  // no record is copied at the back edge: such a copy waits on the record's loads, issued only a round earlier
+  auto prefetch = [&](uint32_t r, Rec& nxr) {
+    nxr = fetch(hn);
+    hn = load_hdr(r + 2 < R ? r + 2 : R - 1);
   };
-  for (uint32_t r = 0; r < R; ++r) {
-    const Rec cur = nx;
-    if (!LCV_FAN_LATE_FETCH) prefetch(r);
+  auto round = [&](const uint32_t r, const Rec& cur, Rec& nxr) __attribute__((always_inline)) {
+    if (!LCV_FAN_LATE_FETCH) prefetch(r, nxr);
     const uint32_t h0 = cur.h0, K = h0 & 15u;
     LCV_FAN_T(0);
     if (active && k < K) {
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
     // LCV_FAN_LATE_FETCH: round r + 1's record loads (and round r + 2's header) are issued here, while the column
     // atomics drain before the barrier (it waits on LDS only), instead of at the top of the round, where a lone wave
     // pays their issue in series with its products; they are still a whole tail ahead of their use
-    if (LCV_FAN_LATE_FETCH) prefetch(r);
+    if (LCV_FAN_LATE_FETCH) prefetch(r, nxr);
     LCV_FAN_T(1);
     __syncthreads();
     LCV_FAN_T(2);
@@ -603,6 +603,11 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
 #endif
     __syncthreads();
     LCV_FAN_T(4);
+  };
+  Rec rb = nx;
+  for (uint32_t r = 0; r < R; r += 2) {
+    round(r, nx, rb);
+    if (r + 1 < R) round(r + 1, rb, nx);
   }
 #if LCV_FAN_X_TIMING
   if (item == 0 && (L == 0 || L == NT - 64))
