@@ -155,7 +155,7 @@ int lcv_set_pipeline(lcv_ctx* ctx, int streams, int chunks);
  *   - both Miller line walks and the accumulation as ONE fan-engine program (lines through LDS), and
  *   - the SSWU maps and the signature decoding on their one-item-per-wave twins (each square-root
  *     product spread over the 64 lanes of a wave).
- * Results are identical to the batch engine's (bit for bit).  Default 64: one update 2.9 ms through
+ * Results are identical to the batch engine's (bit for bit).  Default 64: one update 2.8 ms through
  * lcv_validate_updates on the MI355X (6.0 ms on the batch engine); 0 = the batch engine
  * always.  Performance knob only. */
 int lcv_set_latency_mode(lcv_ctx* ctx, uint64_t max_rows);

@@ -150,7 +150,7 @@ class Verifier:
         programs (hash_to_G2's tail, final exponentiation) on the fan engine (an op's K products on K lanes, its
         reduction and tail on a 16-lane row, one item per block), both Miller walks and the accumulation as one fan-engine program, and the SSWU
         maps / signature decoding one item per wave (square-root chains spread over the wave) — one update
-        6.0 ms on the batch engine -> 2.9 ms.  Results are identical to the batch engine's.  Default 64;
+        6.0 ms on the batch engine -> 2.8 ms.  Results are identical to the batch engine's.  Default 64;
         0 = the batch engine always."""
         self._check(self.lib.lcv_set_latency_mode(self.ctx, int(max_rows)), "lcv_set_latency_mode")
         self.latency_mode = int(max_rows)
