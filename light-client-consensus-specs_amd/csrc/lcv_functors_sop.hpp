@@ -369,6 +369,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F::WAVES))) 
 #ifndef LCV_FAN_X_TIMING
 #define LCV_FAN_X_TIMING 0
 #endif
+#ifndef LCV_FAN_FLAT_COLS
+#define LCV_FAN_FLAT_COLS 1
+#endif
 #ifndef LCV_FAN_FLAT_FETCH
 #define LCV_FAN_FLAT_FETCH 1
 #endif
@@ -437,8 +440,8 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
     const uint32_t off = __builtin_amdgcn_readfirstlane(hd.off);
     const uint32_t words = __builtin_amdgcn_readfirstlane(hd.words);
     c.h3 = __builtin_amdgcn_readfirstlane(hd.h3);
-    c.w = f.P.rec + off + o * words;
-    const uint32_t* wt = f.P.rec + off + (to < T ? to : 0u) * words;  // the tail's op's record
+    c.w = f.P.rec + off + __umul24(o, words);  // (o < 64, words < 2^10: the full-rate 24-bit multiply)
+    const uint32_t* wt = f.P.rec + off + __umul24(to < T ? to : 0u, words);  // the tail's op's record
     const uint32_t K = c.h0 & 15u;
 #if LCV_FAN_FLAT_FETCH
     // branch-free: every lane loads (a lone wave pays each exec-mask region and branch in series).  Product k is
@@ -534,12 +537,23 @@ __global__ __launch_bounds__(lcv_fan_threads<F>()) void k_sop_fan(F f, uint32_t 
         if (K != 0) {
           const uint32_t jj = L & 15u;
           uint64_t lo = 0, hi = 0;
+#if LCV_FAN_FLAT_COLS
+          {  // branch-free: lanes 14, 15 read and zero lane 13's pair again (the reads precede the writes in the wave)
+            const uint32_t jc = jj < 14u ? jj : 13u;
+            const uint64_t cl = racc[jc], ch = racc[jc + 14];
+            racc[jc] = 0;
+            racc[jc + 14] = 0;
+            lo = jj < 14u ? cl : 0ull;
+            hi = jj < 14u ? ch : 0ull;
+          }
+#else
           if (jj < 14u) {
             lo = racc[jj];
             hi = racc[jj + 14];
             racc[jj] = 0;
             racc[jj + 14] = 0;
           }
+#endif
 #if LCV_FAN_X_TIMING > 1
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           LCV_FAN_T(5);
