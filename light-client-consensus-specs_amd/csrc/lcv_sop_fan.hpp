@@ -31,6 +31,9 @@
 #ifndef LCV_FAN_X_CUT  // timing experiments only: 1 no operand reads, 2 no conversion, 3 no multiply-adds, 4 limb-form operands
 #define LCV_FAN_X_CUT 0
 #endif
+#ifndef LCV_FAN_FLAT_TWO
+#define LCV_FAN_FLAT_TWO 1
+#endif
 #ifndef LCV_FAN_PARTS
 #define LCV_FAN_PARTS (LCV_FAN_SPLIT ? 3u : 1u)
 #endif
@@ -96,6 +99,11 @@ LCV_FN void sop_fan_part(int64_t c[13], uint32_t xw, uint32_t yw, uint32_t mk, u
 #endif
 #if LCV_FAN_X_CUT == 1  // timing experiments only (wrong results): no operand reads
   LCV_UNROLL for (int j = 0; j < 12; ++j) { Xw[j] = xw * (j + 1); Yw[j] = yw + j; }
+#elif LCV_FAN_FLAT_TWO
+  // a one-term operand's second handle is the zero slot (tools/gen_sop.py asserts it), so when any product of the
+  // round has a two-term X (or Y) — a wave-uniform test — every lane adds its second term: no exec-mask region
+  sop_operand(Xw, xw, (masks & 0xFFFFu) != 0u, base);
+  sop_operand(Yw, yw, (masks >> 16) != 0u, base);
 #else
   sop_operand(Xw, xw, (masks >> k) & 1u, base);
   sop_operand(Yw, yw, (masks >> (16 + k)) & 1u, base);
